@@ -1,0 +1,92 @@
+/*
+ * render.h -- C ABI of the MI355X rasterizer (librender.so, also installed as render.dylib).
+ *
+ * Drop-in for the reference's dylib boundary:
+ *   struct layouts      /root/reference/render-cpp/render.hpp:7-21 (PixelData 24 B, Input 24 B)
+ *   updateAndRender     /root/reference/render-cpp/render.cpp:264-265, bound by the Swift main loop
+ *                       with dlopen + dlsym("updateAndRender") (main.swift:96-98) and called once per
+ *                       60 Hz tick (main.swift:121).
+ * Everything else (s3r_*) is an extension the reference does not have; a caller that only uses
+ * updateAndRender sees the reference's behaviour: lazy init from data.bin found next to the library
+ * (render.cpp:160-176, exit(666) if missing), the same camera and resize semantics, and the full
+ * frame written into pixel_data->buffer before the call returns.
+ */
+#ifndef S3R_RENDER_H
+#define S3R_RENDER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* render.hpp:7-13 */
+typedef struct {
+    uint32_t *buffer;       /* caller-owned host buffer, 0x00RRGGBB, row-major, stride = width */
+    uint32_t width;
+    uint32_t height;
+    uint32_t bytesPerPixel; /* 4 */
+    uint32_t bufferSize;    /* bytes; 4 * width * height (main.swift:163) */
+} PixelData;
+
+/* simd_float2: 8 bytes, 8-byte aligned */
+typedef struct __attribute__((aligned(8))) { float x, y; } s3r_float2;
+
+/* render.hpp:15-21 */
+typedef struct {
+    float up;
+    float down;
+    float left;
+    float right;
+    s3r_float2 mouse;
+} Input;
+
+/* Replaces render.cpp:264-384.  Renders one frame on the GPU into pixel_data->buffer. */
+void updateAndRender(const PixelData *pixel_data, const Input *input);
+
+/* ---------------- extensions (not in the reference) ---------------- */
+
+/* Use `data_path` (NULL: the reference's dladdr search) on HIP device `device` (-1: the calling
+ * thread's current device) and drop all state so the next call re-initialises like a first call.
+ * Environment overrides: S3R_DATA_PATH, S3R_DEVICE.  Returns 0. */
+int s3r_configure(const char *data_path, int device);
+
+/* Release every GPU resource and registered host buffer; the next call re-initialises. */
+void s3r_shutdown(void);
+
+/* One frame for one part of an interleaved row-band split (multi-GPU).  Same camera / init /
+ * resize semantics as updateAndRender.  Frame row y belongs to part ((y / band_rows) % n_parts);
+ * this part's rows are written compactly, in increasing y, to the DEVICE buffer dev_out
+ * (rows_local x width u32), asynchronously on `stream` (a hipStream_t; NULL = the library's own
+ * stream).  n_parts = 1 renders the whole frame.  Returns rows_local, or -1 on bad arguments. */
+int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height, uint32_t band_rows,
+                         uint32_t n_parts, uint32_t part, uint32_t *dev_out, void *stream);
+
+/* Rows of a height-row frame owned by `part`. */
+uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);
+
+/* Device-side timing: with enable != 0 every frame records HIP events on its stream around the
+ * fragment kernel and around the whole frame.  s3r_timing_collect synchronises, writes
+ * out[0] = summed fragment-kernel ms, out[1] = summed frame ms, out[2] = frames, and resets. */
+void s3r_timing(int enable);
+void s3r_timing_collect(double out[3]);
+
+/* Scene counts after init: out = {vertices, indices, attributes, texels, triangle slots, 0, 0, 0}. */
+void s3r_scene_counts(uint64_t out[8]);
+
+/* Copy the current camera matrix (3 rows x 4) and raster factor. */
+void s3r_camera(float out_matrix[12], float *out_factor);
+
+/* Self-test hooks (tests only): out[i] = the float32 value after n[i] sequential steps
+ * s = fl(s + d) (the render.cpp:374/:378 walk) computed by the library's O(binades) walker;
+ * lin[i]/del[i] = whether n[i] consecutive walk values are s + k*del exactly. */
+void s3r_selftest_walk_host(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin,
+                            float *del, uint64_t count);
+int s3r_selftest_walk_device(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin,
+                             float *del, uint32_t count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,423 @@
+// render_api.cpp -- the C-ABI shim: what render.cpp's host side did, with the per-pixel work moved
+// to the gfx950 kernels (kernels.hip).
+//
+//   updateAndRender   render.cpp:264-384   lazy init, camera update, resize, frame, copy-out
+//   initialize        render.cpp:160-210   data.bin search next to the library (dladdr), load, upload
+//   update_camera     render.cpp:134-156   host float32, same operation order as the reference
+//
+// State is process-global like the reference's statics (render.cpp:51-113); calls are expected from
+// one thread at a time (main.swift calls from its main-thread timer only).
+#include <dlfcn.h>
+#include <limits.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/render.h"
+#include "s3r_kernels.h"
+
+using namespace s3r;
+
+#define HIPCHECK(x)                                                                                   \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) {                                                                       \
+            fprintf(stderr, "s3r: HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), __FILE__,        \
+                    __LINE__, #x);                                                                    \
+            abort();                                                                                  \
+        }                                                                                             \
+    } while (0)
+
+namespace {
+
+struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
+
+struct Lib {
+    bool initialized = false;
+    std::string data_path;     // "" = reference search
+    int device = -1;
+
+    // camera state, render.cpp:51-65
+    F3 pos{0, 0, 0}, ax{1, 0, 0}, ay{0, 1, 0}, az{0, 0, 1};
+    Mat34 m{{{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}}};
+    float mouse[2] = {0, 0};
+    // config, render.cpp:81-97
+    float factor = 1;
+    uint32_t depth_buffer_size = 0;
+
+    // scene on the device
+    uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
+    uint64_t nindices = 0;
+    float4 *vtx = nullptr, *nrm = nullptr, *pay = nullptr;
+    uint8_t *disc = nullptr;
+    uint32_t *vidx = nullptr, *aidx = nullptr, *tex = nullptr;
+    // per-frame scratch
+    float4 *cv = nullptr, *rv = nullptr, *ncam = nullptr;
+    TriSetup *tris = nullptr;
+    uint32_t *frame = nullptr;
+    size_t frame_cap = 0;
+    hipStream_t stream = nullptr;
+
+    // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
+    struct Reg { void *p; size_t n; bool ok; };
+    std::vector<Reg> regs;
+
+    bool timing = false;
+    std::vector<TimingSlot> tslots;
+    size_t tcount = 0;
+};
+
+Lib g;
+
+float config_scale() {
+    const float fov = (float)M_PI / 5.f;        // render.cpp:91
+    return kNear * tanf(fov / 2);               // render.cpp:92
+}
+
+// ---------------------------------------------------------------- camera, render.cpp:134-156
+F3 smul3(float s, F3 a) { return mk3(s * a.x, s * a.y, s * a.z); }
+F3 cross3(F3 a, F3 b) { return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+// simd_act(q, v) = v + re*t + cross(im, t), t = 2*cross(im, v)
+F3 quat_act(F3 im, float re, F3 v) {
+    const F3 t = smul3(2.0f, cross3(im, v));
+    return add3(add3(v, smul3(re, t)), cross3(im, t));
+}
+
+void update_camera(const Input *in, bool force) {
+    bool changed = false;
+    if (in->left > 0 || in->right > 0 || in->up > 0 || in->down > 0) {
+        changed = true;
+        const F3 mv = add3(smul3(in->right - in->left, g.ax), smul3(in->down - in->up, g.az));
+        g.pos = add3(g.pos, smul3(kSpeed, mv));
+    }
+    if (in->mouse.x != g.mouse[0] || in->mouse.y != g.mouse[1]) {
+        changed = true;
+        const F3 d = add3(add3(smul3(g.mouse[0] - in->mouse.x, g.ax), smul3(g.mouse[1] - in->mouse.y, g.ay)),
+                          smul3(100 / kRotationSpeed, g.az));
+        const F3 z = fast_normalize3(d);
+        // simd_quaternion(az, z): dot(az, z) > 0 always here, so the reduced form applies
+        const F3 h = fast_normalize3(add3(g.az, z));
+        const F3 im = cross3(g.az, h);
+        const float re = dot3(g.az, h);
+        g.ax = fast_normalize3(quat_act(im, re, g.ax));
+        g.ay = fast_normalize3(quat_act(im, re, g.ay));
+        g.az = z;
+        g.mouse[0] = in->mouse.x;
+        g.mouse[1] = in->mouse.y;
+    }
+    if (changed || force) {
+        const F3 r[3] = {g.ax, g.ay, g.az};
+        for (int i = 0; i < 3; i++) {
+            g.m.m[i][0] = r[i].x; g.m.m[i][1] = r[i].y; g.m.m[i][2] = r[i].z;
+            g.m.m[i][3] = -dot3(r[i], g.pos);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- data.bin, render.cpp:160-210
+std::string find_data_path() {
+    if (const char *e = getenv("S3R_DATA_PATH")) return e;
+    if (!g.data_path.empty()) return g.data_path;
+    Dl_info info;
+    if (dladdr((const void *)updateAndRender, &info) && info.dli_fname) {
+        std::string lib = info.dli_fname;
+        const size_t slash = lib.rfind('/');
+        const std::string dir = slash == std::string::npos ? "." : lib.substr(0, slash);
+        for (const char *suffix : {"/data.bin", "/Resources/data.bin", "/../data-generator/data.bin"}) {
+            const std::string p = dir + suffix;
+            if (FILE *f = fopen(p.c_str(), "rb")) { fclose(f); return p; }
+        }
+    }
+    return "";
+}
+
+template <class T> T *dalloc(size_t n) {
+    T *p = nullptr;
+    HIPCHECK(hipMalloc((void **)&p, (n ? n : 1) * sizeof(T)));
+    return p;
+}
+
+[[noreturn]] void bad_scene(const std::string &path, const char *why) {
+    fprintf(stderr, "s3r: %s: malformed data.bin (%s)\n", path.c_str(), why);
+    exit(666);
+}
+
+void initialize() {
+    const std::string path = find_data_path();
+    FILE *fp = path.empty() ? nullptr : fopen(path.c_str(), "rb");
+    if (!fp) exit(666);                                                 // render.cpp:173
+    auto rd = [&](void *dst, size_t bytes) {
+        if (bytes && fread(dst, 1, bytes, fp) != bytes) bad_scene(path, "truncated");
+    };
+    uint64_t cnt[2];
+    rd(cnt, 16);
+    const uint64_t nv = cnt[0];
+    std::vector<float4> vtx(nv);
+    rd(vtx.data(), nv * 16);
+    rd(cnt, 16);
+    const uint64_t ni = cnt[0];
+    std::vector<int64_t> vi(ni + ni % 2);
+    rd(vi.data(), vi.size() * 8);
+    rd(cnt, 16);
+    const uint64_t na = cnt[0];
+    std::vector<uint8_t> attr(na * 48);
+    rd(attr.data(), attr.size());
+    rd(cnt, 16);
+    const uint64_t nai = cnt[0];
+    std::vector<int64_t> ai(nai + nai % 2);
+    rd(ai.data(), ai.size() * 8);
+    rd(cnt, 16);
+    const uint64_t nt = cnt[0];
+    std::vector<uint32_t> tex(nt);
+    rd(tex.data(), nt * 4);
+    fclose(fp);
+
+    // The reference trusts the file; the GPU must not read out of bounds, so check it here.
+    if (nv >= (1ull << 32) || na >= (1ull << 32) || nt >= (1ull << 32)) bad_scene(path, "too large");
+    if (nai < ni) bad_scene(path, "fewer attribute indices than vertex indices");
+    const uint64_t ntri = ni / 3;
+    std::vector<uint32_t> vi32(3 * ntri), ai32(3 * ntri);
+    for (uint64_t k = 0; k < 3 * ntri; k++) {
+        if (vi[k] < 0 || (uint64_t)vi[k] >= nv) bad_scene(path, "vertex index out of range");
+        if (ai[k] < 0 || (uint64_t)ai[k] >= na) bad_scene(path, "attribute index out of range");
+        vi32[k] = (uint32_t)vi[k];
+        ai32[k] = (uint32_t)ai[k];
+    }
+    std::vector<float4> nrm(na), pay(na);
+    std::vector<uint8_t> disc(na);
+    for (uint64_t k = 0; k < na; k++) {
+        memcpy(&nrm[k], &attr[48 * k], 16);
+        memcpy(&pay[k], &attr[48 * k + 16], 16);
+        uint32_t d;
+        memcpy(&d, &attr[48 * k + 32], 4);                              // disc_t at +32
+        disc[k] = d != 0;
+    }
+
+    if (g.device < 0) {
+        if (const char *e = getenv("S3R_DEVICE")) g.device = atoi(e);
+        else HIPCHECK(hipGetDevice(&g.device));
+    }
+    HIPCHECK(hipSetDevice(g.device));
+    if (!g.stream) HIPCHECK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
+    g.nindices = ni;
+    g.vtx = dalloc<float4>(nv); g.nrm = dalloc<float4>(na); g.pay = dalloc<float4>(na);
+    g.disc = dalloc<uint8_t>(na);
+    g.vidx = dalloc<uint32_t>(3 * ntri); g.aidx = dalloc<uint32_t>(3 * ntri);
+    g.tex = dalloc<uint32_t>(nt);
+    g.cv = dalloc<float4>(nv); g.rv = dalloc<float4>(nv); g.ncam = dalloc<float4>(na);
+    g.tris = dalloc<TriSetup>(2 * ntri);
+    HIPCHECK(hipMemcpy(g.vtx, vtx.data(), nv * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.nrm, nrm.data(), na * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.pay, pay.data(), na * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.disc, disc.data(), na, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.vidx, vi32.data(), 12 * ntri, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.aidx, ai32.data(), 12 * ntri, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(g.tex, tex.data(), nt * 4, hipMemcpyHostToDevice));
+}
+
+void unregister_all() {
+    for (auto &r : g.regs)
+        if (r.ok) (void)hipHostUnregister(r.p);
+    g.regs.clear();
+}
+
+void release_all() {
+    if (g.initialized) {
+        (void)hipSetDevice(g.device);
+        if (g.stream) (void)hipStreamSynchronize(g.stream);
+        unregister_all();
+        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.cv, g.rv, g.ncam, g.tris, g.frame};
+        for (void *p : ptrs)
+            if (p) (void)hipFree(p);
+        for (auto &t : g.tslots) {
+            (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
+        }
+        if (g.stream) (void)hipStreamDestroy(g.stream);
+    }
+    const std::string path = g.data_path;
+    const int dev = g.device;
+    g.~Lib();
+    new (&g) Lib();
+    g.data_path = path;
+    g.device = dev;
+}
+
+// render.cpp:266-280: first-call init, camera, resize.
+void frame_begin(const Input *input, uint32_t width, uint32_t height) {
+    if (!g.initialized) {
+        g.initialized = true;
+        initialize();
+        update_camera(input, true);
+    } else {
+        update_camera(input, false);
+        HIPCHECK(hipSetDevice(g.device));
+    }
+    const uint32_t dbs = width * height * (uint32_t)sizeof(float);
+    if (g.depth_buffer_size != dbs) {
+        g.depth_buffer_size = dbs;
+        g.factor = kNear * (float)height / (2 * config_scale());          // render.cpp:279
+        unregister_all();
+    }
+}
+
+TimingSlot *timing_slot() {
+    if (!g.timing) return nullptr;
+    if (g.tcount == g.tslots.size()) {
+        TimingSlot t;
+        HIPCHECK(hipEventCreate(&t.frame0)); HIPCHECK(hipEventCreate(&t.frag0)); HIPCHECK(hipEventCreate(&t.frag1));
+        g.tslots.push_back(t);
+    }
+    return &g.tslots[g.tcount++];
+}
+
+void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                 uint32_t *out, hipStream_t st) {
+    TimingSlot *ts = timing_slot();
+    if (ts) HIPCHECK(hipEventRecord(ts->frame0, st));
+    const float sw = (float)W, sh = (float)H;
+    launch_vertex(g.vtx, g.nv, g.nrm, g.na, g.m, g.factor, sw, sh, g.cv, g.rv, g.ncam, st);
+    launch_setup(g.cv, g.rv, g.ncam, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.factor, sw, sh, g.tris, st);
+    if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
+    launch_fragment(g.tris, 2 * g.ntri, g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
+    if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
+    HIPCHECK(hipGetLastError());
+}
+
+bool host_pinned(void *p, size_t n) {
+    for (auto &r : g.regs)
+        if (r.p == p && r.n == n) return r.ok;
+    if (getenv("S3R_NO_PIN")) return false;
+    if (g.regs.size() >= 4) unregister_all();
+    const bool ok = hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    g.regs.push_back({p, n, ok});
+    return ok;
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) void updateAndRender(const PixelData *pixel_data, const Input *input) {
+    const uint32_t W = pixel_data->width, H = pixel_data->height;
+    frame_begin(input, W, H);
+    const size_t npx = (size_t)W * H;
+    if (g.frame_cap < npx) {
+        if (g.frame) HIPCHECK(hipFree(g.frame));
+        g.frame = dalloc<uint32_t>(npx);
+        g.frame_cap = npx;
+    }
+    if (npx) render_core(W, H, H ? H : 1, 1, 0, H, g.frame, g.stream);
+    // memset_pattern4 fills bufferSize bytes (render.cpp:282); the frame covers W*H pixels.
+    const size_t frame_bytes = npx * 4;
+    const size_t copy_bytes = pixel_data->bufferSize < frame_bytes ? pixel_data->bufferSize : frame_bytes;
+    if (copy_bytes) {
+        host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        HIPCHECK(hipMemcpyAsync(pixel_data->buffer, g.frame, copy_bytes, hipMemcpyDeviceToHost, g.stream));
+    }
+    for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
+    HIPCHECK(hipStreamSynchronize(g.stream));
+}
+
+__attribute__((visibility("default"))) int s3r_configure(const char *data_path, int device) {
+    release_all();
+    g.data_path = data_path ? data_path : "";
+    g.device = device;
+    return 0;
+}
+
+__attribute__((visibility("default"))) void s3r_shutdown(void) { release_all(); }
+
+__attribute__((visibility("default"))) uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows,
+                                                                   uint32_t n_parts, uint32_t part) {
+    if (band_rows == 0 || n_parts == 0 || part >= n_parts) return 0;
+    uint32_t rows = 0;
+    for (uint64_t b = part; b * band_rows < height; b += n_parts) {
+        const uint64_t y0 = b * band_rows;
+        rows += (uint32_t)((height - y0) < band_rows ? (height - y0) : band_rows);
+    }
+    return rows;
+}
+
+__attribute__((visibility("default"))) int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height,
+                                                               uint32_t band_rows, uint32_t n_parts, uint32_t part,
+                                                               uint32_t *dev_out, void *stream) {
+    if (band_rows == 0 || n_parts == 0 || part >= n_parts || (!dev_out && width && height)) return -1;
+    frame_begin(input, width, height);
+    const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
+    hipStream_t st = stream ? (hipStream_t)stream : g.stream;
+    if (rows && width) render_core(width, height, band_rows, n_parts, part, rows, dev_out, st);
+    return rows;
+}
+
+__attribute__((visibility("default"))) void s3r_timing(int enable) {
+    g.timing = enable != 0;
+    g.tcount = 0;
+}
+
+__attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
+    double frag = 0, frame = 0;
+    for (size_t i = 0; i < g.tcount; i++) {
+        float a = 0, b = 0;
+        HIPCHECK(hipEventSynchronize(g.tslots[i].frag1));
+        HIPCHECK(hipEventElapsedTime(&a, g.tslots[i].frag0, g.tslots[i].frag1));
+        HIPCHECK(hipEventElapsedTime(&b, g.tslots[i].frame0, g.tslots[i].frag1));
+        frag += a;
+        frame += b;
+    }
+    out[0] = frag;
+    out[1] = frame;
+    out[2] = (double)g.tcount;
+    g.tcount = 0;
+}
+
+__attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
+    out[0] = g.nv; out[1] = g.nindices; out[2] = g.na; out[3] = g.ntex; out[4] = 2ull * g.ntri;
+    out[5] = out[6] = out[7] = 0;
+}
+
+__attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {
+    memcpy(out_matrix, g.m.m, sizeof g.m.m);
+    if (out_factor) *out_factor = g.factor;
+}
+
+// ---- self-test hooks: the exact repeated-addition walker on the host and on the device ----
+__attribute__((visibility("default"))) void s3r_selftest_walk_host(const float *s, const float *d, const uint32_t *n,
+                                                                  float *out, uint32_t *lin, float *del,
+                                                                  uint64_t count) {
+    for (uint64_t i = 0; i < count; i++) {
+        out[i] = exact_walk(s[i], d[i], n[i]);
+        lin[i] = chunk_linear(s[i], d[i], n[i], &del[i]) ? 1u : 0u;
+    }
+}
+
+__attribute__((visibility("default"))) int s3r_selftest_walk_device(const float *s, const float *d, const uint32_t *n,
+                                                                   float *out, uint32_t *lin, float *del,
+                                                                   uint32_t count) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    float *ds, *dd, *dout, *ddel;
+    uint32_t *dn, *dlin;
+    const size_t b = (size_t)count * 4;
+    HIPCHECK(hipMalloc((void **)&ds, b + 4)); HIPCHECK(hipMalloc((void **)&dd, b + 4));
+    HIPCHECK(hipMalloc((void **)&dn, b + 4)); HIPCHECK(hipMalloc((void **)&dout, b + 4));
+    HIPCHECK(hipMalloc((void **)&dlin, b + 4)); HIPCHECK(hipMalloc((void **)&ddel, b + 4));
+    HIPCHECK(hipMemcpy(ds, s, b, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dd, d, b, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(dn, n, b, hipMemcpyHostToDevice));
+    launch_walk_test(ds, dd, dn, dout, dlin, ddel, count, nullptr);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpy(out, dout, b, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(lin, dlin, b, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(del, ddel, b, hipMemcpyDeviceToHost));
+    void *ptrs[] = {ds, dd, dn, dout, dlin, ddel};
+    for (void *p : ptrs) HIPCHECK(hipFree(p));
+    return 0;
+}
+
+}  // extern "C"

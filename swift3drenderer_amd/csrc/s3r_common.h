@@ -1,0 +1,150 @@
+// s3r_common.h -- types and exact float32 arithmetic shared by the host shim and the gfx950 kernels.
+//
+// Reference: /root/reference/render-cpp/render.cpp (sarastro-nl/Swift3DRenderer).  Every float
+// operation here is ONE IEEE binary32 op in the order render.cpp evaluates it; the library is built
+// with -ffp-contract=off and without fast-math so hipcc emits no FMA and keeps IEEE div/sqrt.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define S3R_HD __host__ __device__ __forceinline__
+
+namespace s3r {
+
+constexpr float kNear = 0.1f;                                  // render.cpp:90
+constexpr float kSpeed = 0.1f;                                 // render.cpp:94
+constexpr float kRotationSpeed = 0.3f;                         // render.cpp:95
+constexpr uint32_t kBackground = (30u << 16) | (30u << 8) | 30u;  // RGB(30,30,30), render.cpp:96
+constexpr uint32_t kTexTexels = 1u << 18;                      // 512 x 512 per texture, render.cpp:347
+constexpr uint32_t kInvalidK = 0xFFFFFFFFu;
+
+enum : uint32_t { kDead = 0, kColour = 1, kTexture = 2 };
+
+// One triangle after gather / clip / cull / raster setup (render.cpp:297-359).  The frame's
+// triangle list has 2T slots: slot t = original triangle t, slot T+t = the triangle clip() appended
+// while processing t (render.cpp:239-257).  Slot order == the reference's processing order, which
+// decides depth ties (strict '>' at render.cpp:364).
+struct alignas(16) TriSetup {
+    uint32_t kind, xmin, xmax, ymin;
+    uint32_t ymax, tex_base, pad0, pad1;
+    float ws[4];     // wstart (render.cpp:324)
+    float dx[4];     // per-pixel step (render.cpp:327)
+    float dy[4];     // per-row step (render.cpp:328)
+    float rvz[4];    // 1/z per vertex (render.cpp:336)
+    float cvr[12];   // cv_i * rvz_i, 3 x float4 (render.cpp:337)
+    float nr[12];    // n_i * rvz_i (render.cpp:338)
+    float col[12];   // colour: cc_i (render.cpp:342);  texture: uv0 uv1 | uv2 dz | tpp (render.cpp:348-352)
+};
+static_assert(sizeof(TriSetup) == 240, "TriSetup layout");
+
+// Camera matrix as rows (simd_matrix_from_rows, render.cpp:152-154).
+struct Mat34 { float m[3][4]; };
+
+S3R_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+S3R_HD float u2f(uint32_t x) { return __builtin_bit_cast(float, x); }
+S3R_HD uint32_t fexp(float x) { return (f2u(x) >> 23) & 0xFFu; }
+S3R_HD float pow2_biased(uint32_t e) { return u2f(e << 23); }   // 2^(e-127), e in [1, 254]
+S3R_HD bool is_finite(float x) { return fexp(x) != 0xFFu; }
+
+S3R_HD float quot_approx(float num, float den) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return num * __builtin_amdgcn_rcpf(den);   // ~1 ulp; every use below is re-checked exactly
+#else
+    return num / den;
+#endif
+}
+
+// exact_walk(s, d, n) == the float32 value after n sequential steps s = fl(s + d)
+// (render.cpp:374 `weight.w += weight.dx`, :378 `weight.wy += weight.dy`), in O(binades) work.
+//
+// Inside one binade [2^e, 2^(e+1)) every sum s + d rounds onto the grid u = 2^(e-23), and the step
+// fl(s + d) - s is the same for every s there (for a d exactly half-way between grid points the
+// tie-to-even parity settles after at most one step).  So once two consecutive steps are equal and
+// stay in the binade, j more steps are s + j*delta, exactly representable, as long as the last
+// sum stays 2 steps clear of the binade edge.  Near zero (|s| < 4|d|, or < 8|d| heading towards
+// zero) and at binade edges we take single steps.  Validated against the sequential loop
+// (tests/test_exact_walk.py).
+S3R_HD float exact_walk(float s, float d, uint32_t n) {
+    if (n == 0) return s;
+    const float ad = fabsf(d);
+    if (ad == 0.0f || !is_finite(s) || !is_finite(d)) return s + d;   // one add is a fixed point
+    while (n) {
+        const float as = fabsf(s);
+        const bool towards_zero = (s < 0.0f) != (d < 0.0f);
+        if (!(as >= 4.0f * ad) || (towards_zero && as < 8.0f * ad)) { s = s + d; --n; continue; }
+        const float s1 = s + d;
+        if (n == 1) return s1;
+        const float s2 = s1 + d;
+        const uint32_t e = fexp(s);
+        if (e == 0u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - s) != (s2 - s1)) {
+            s = s1; --n; continue;
+        }
+        const float delta = s1 - s;           // exact (same binade)
+        if (delta == 0.0f) return s;          // fl(s + d) == s: stagnated for good
+        const float adel = fabsf(delta);
+        const bool away = (s > 0.0f) == (delta > 0.0f);
+        const float room = away ? pow2_biased(e + 1) - as : as - pow2_biased(e);   // exact (Sterbenz)
+        const float q = quot_approx(room, adel);
+        uint32_t j = q >= 3.0f ? (uint32_t)q - 2u : 0u;
+        // valid iff (j + 2) * |delta| <= room; the product is exact whenever it is <= room
+        while (j > 0u && (float)(j + 2u) * adel > room) --j;
+        if (j < 2u) { s = s1; --n; continue; }
+        if (j > n) j = n;
+        s = s + (float)j * delta;             // exact: lands on the grid inside the binade
+        n -= j;
+    }
+    return s;
+}
+
+// True when the m values S(c, d, k), k = 0..m-1, are exactly c + k*delta (one binade, constant
+// step); *delta receives the step.  This is exact_walk's jump test applied to a chunk of m pixels.
+S3R_HD bool chunk_linear(float c, float d, uint32_t m, float *delta) {
+    *delta = 0.0f;
+    if (m <= 1u) return true;
+    const float ad = fabsf(d);
+    if (!is_finite(c) || !is_finite(d)) return false;
+    if (ad == 0.0f) return c != 0.0f;                     // c + 0 == c unless c is -0
+    const float ac = fabsf(c);
+    const bool towards_zero = (c < 0.0f) != (d < 0.0f);
+    if (!(ac >= 4.0f * ad) || (towards_zero && ac < 8.0f * ad)) return false;
+    const float s1 = c + d, s2 = s1 + d;
+    const uint32_t e = fexp(c);
+    if (e == 0u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - c) != (s2 - s1)) return false;
+    const float del = s1 - c;
+    *delta = del;
+    if (del == 0.0f) return true;
+    const float adel = fabsf(del);
+    const bool away = (c > 0.0f) == (del > 0.0f);
+    const float room = away ? pow2_biased(e + 1) - ac : ac - pow2_biased(e);
+    return (float)(m + 1u) * adel <= room;                // jump of m-1 steps is valid
+}
+
+// ---- float3 helpers in the reference's evaluation order ----
+struct F3 { float x, y, z; };
+S3R_HD F3 mk3(float x, float y, float z) { return F3{x, y, z}; }
+S3R_HD F3 add3(F3 a, F3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+S3R_HD F3 muls3(F3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+S3R_HD float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }   // simd_dot
+S3R_HD F3 fast_normalize3(F3 a) { return muls3(a, 1.0f / sqrtf(dot3(a, a))); }  // simd_fast_normalize
+
+// (uint8_t)(float) as x86 computes it: cvttss2si to int32 (0x80000000 when out of range or NaN),
+// then the low byte (render.cpp:8 RGB macro).
+S3R_HD uint32_t u8_of_float(float f) {
+    const int32_t i = (fabsf(f) < 2147483648.0f) ? (int32_t)f : (int32_t)0x80000000;
+    return (uint32_t)i & 0xFFu;
+}
+S3R_HD uint32_t rgb_pack(float r, float g, float b) {
+    return (u8_of_float(r) << 16) + (u8_of_float(g) << 8) + u8_of_float(b);
+}
+// (uint32_t)(float) for |f| < 2^31 (render.cpp:126-129, :319-322): truncation, low 32 bits.
+S3R_HD uint32_t u32_of_float(float f) {
+    return (fabsf(f) < 2147483648.0f) ? (uint32_t)(int32_t)f : 0u;
+}
+// render.cpp:115-122
+S3R_HD uint32_t next_power_of_two(uint32_t i) {
+    i--; i |= i >> 1; i |= i >> 2; i |= i >> 4; return i + 1;
+}
+// fmodf(x, 1) for the ripmap (render.cpp:128-129): x - trunc(x) is exact for every finite x.
+S3R_HD float frac1(float x) { return x - truncf(x); }
+
+}  // namespace s3r

@@ -1,0 +1,26 @@
+// s3r_kernels.h -- host-callable launchers for the gfx950 kernels (kernels.hip).
+#pragma once
+#include "s3r_common.h"
+
+namespace s3r {
+
+void launch_vertex(const float4 *vtx, uint32_t nv, const float4 *nrm, uint32_t na, const Mat34 &m,
+                   float factor, float sw, float sh, float4 *cv, float4 *rv, float4 *ncam, hipStream_t st);
+
+void launch_setup(const float4 *cv, const float4 *rv, const float4 *ncam, const float4 *pay,
+                  const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
+                  float factor, float sw, float sh, TriSetup *tris, hipStream_t st);
+
+// Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
+// (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
+// out[lr * W + x].
+void launch_fragment(const TriSetup *tris, uint32_t nslots, const uint32_t *tex, uint32_t ntex, uint32_t *out,
+                     uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                     hipStream_t st);
+
+uint32_t fragment_segment_pixels();
+
+void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,
+                      uint32_t count, hipStream_t st);
+
+}  // namespace s3r

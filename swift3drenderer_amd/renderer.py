@@ -1,0 +1,122 @@
+"""Host-side mirror of the reference's plugin interface: ``updateAndRender(PixelData*, Input*)``.
+
+This loads the in-tree gfx950 library (``librender.so``) and calls it through its C ABI exactly
+the way the Swift main loop does (``main.swift:96-98`` dlopen/dlsym, ``:121`` the call).  There is
+no CPU fallback: if the library is missing or cannot be loaded this raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .abi import Input, pixel_data_for
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, 'librender.so')
+
+EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_render_bands', 's3r_band_rows_local',
+           's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen the rasterizer (RTLD_NOW, like main.swift:96) and declare its C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f'{path} is missing: run __graft_entry__.build() (no CPU fallback exists)')
+    lib = ctypes.CDLL(path, mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    lib.updateAndRender.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.updateAndRender.restype = None
+    lib.s3r_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.s3r_configure.restype = ctypes.c_int
+    lib.s3r_shutdown.argtypes = []
+    lib.s3r_render_bands.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    lib.s3r_render_bands.restype = ctypes.c_int64
+    lib.s3r_band_rows_local.argtypes = [ctypes.c_uint32] * 4
+    lib.s3r_band_rows_local.restype = ctypes.c_uint32
+    lib.s3r_timing.argtypes = [ctypes.c_int]
+    lib.s3r_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double)]
+    lib.s3r_scene_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    lib.s3r_camera.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    _lib = lib
+    return lib
+
+
+def band_rows_local(height: int, band: int, nparts: int, part: int) -> int:
+    return int(load_library().s3r_band_rows_local(height, band, nparts, part))
+
+
+def band_row_ids(height: int, band: int, nparts: int, part: int) -> np.ndarray:
+    """Frame rows owned by `part`, in the order they are stored locally."""
+    y = np.arange(height)
+    return y[(y // band) % nparts == part]
+
+
+class Renderer:
+    """Stateful like the reference: one scene, one camera, lazy init on the first call."""
+
+    def __init__(self, data_path: str | None = None, device: int = -1):
+        self.lib = load_library()
+        self.configure(data_path, device)
+
+    def configure(self, data_path: str | None, device: int = -1):
+        self.lib.s3r_configure(data_path.encode() if data_path else None, device)
+
+    def update_and_render(self, width: int, height: int, inp, out: np.ndarray | None = None) -> np.ndarray:
+        """updateAndRender into a host uint32 (H, W) buffer (the reference's contract)."""
+        if out is None:
+            out = np.empty((height, width), dtype=np.uint32)
+        pd = pixel_data_for(out)
+        i = Input.of(inp)
+        self.lib.updateAndRender(ctypes.byref(pd), ctypes.byref(i))
+        return out
+
+    def render_bands(self, inp, width: int, height: int, band: int, nparts: int, part: int, dev_ptr: int,
+                     stream: int = 0) -> int:
+        """Render one part of an interleaved row-band split into device memory at dev_ptr."""
+        i = Input.of(inp)
+        r = self.lib.s3r_render_bands(ctypes.byref(i), width, height, band, nparts, part,
+                                      ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None))
+        if r < 0:
+            raise ValueError('s3r_render_bands: bad arguments')
+        return int(r)
+
+    def timing(self, enable: bool):
+        self.lib.s3r_timing(1 if enable else 0)
+
+    def timing_collect(self):
+        out = (ctypes.c_double * 3)()
+        self.lib.s3r_timing_collect(out)
+        return out[0], out[1], int(out[2])
+
+    def scene_counts(self):
+        out = (ctypes.c_uint64 * 8)()
+        self.lib.s3r_scene_counts(out)
+        return list(out)
+
+    def camera(self):
+        m = (ctypes.c_float * 12)()
+        f = ctypes.c_float()
+        self.lib.s3r_camera(m, ctypes.byref(f))
+        return np.array(m, dtype=np.float32).reshape(3, 4), f.value
+
+    def shutdown(self):
+        self.lib.s3r_shutdown()
+
+
+def render_pose(r: Renderer, data_path: str, pose_script, width: int, height: int, extra_frames: int = 0):
+    """Fresh state, run a pose script, return the last frame (mirrors oracle.render_pose)."""
+    r.configure(data_path)
+    out = None
+    for t in pose_script:
+        out = r.update_and_render(width, height, t)
+    hold = (0, 0, 0, 0) + tuple(pose_script[-1][4:6])
+    for _ in range(extra_frames):
+        out = r.update_and_render(width, height, hold)
+    return out
