@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s and Mpixels/s of updateAndRender's frame at 3840x2160 on the packaged scene.
+
+Step = one frame of the hot path (render.cpp:264-384): camera update, vertex transform, triangle
+setup/clip/cull, fragment stage, with the frame left in device memory (HBM-resident value; the
+PCIe-inclusive updateAndRender rate is reported separately as `e2e`).  With N GPUs the frame's
+rows are split into interleaved bands (band g -> rank g % N), every rank renders its bands and one
+RCCL gather (torch.distributed over nccl) reassembles the frame on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = 'frames/sec + Mpixels/s at 3840x2160, data.bin scene; 1/2/4/8-GPU scaling'
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md, HBM3E peak (spec)
+TRI_SETUP_BYTES = 240    # sizeof(TriSetup)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=200)
+    p.add_argument('--warmup', type=int, default=20)
+    p.add_argument('--width', type=int, default=3840)
+    p.add_argument('--height', type=int, default=2160)
+    p.add_argument('--scene', default='full')
+    p.add_argument('--pose', default='P_over')
+    p.add_argument('--band', type=int, default=16, help='rows per interleaved band (multi-GPU)')
+    p.add_argument('--cpu-seconds', type=float, default=10.0, help='CPU-baseline sample budget')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-e2e', action='store_true')
+    return p.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(['lscpu'], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            if line.startswith('Model name'):
+                return line.split(':', 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or 'unknown'
+
+
+def cpu_baseline(data_path, script, hold, w, h, budget_s):
+    """The CPU oracle (a single-threaded C restatement of render.cpp) on this host, bounded sample."""
+    from oracle.oracle import OracleRenderer
+    r = OracleRenderer(data_path)
+    for t in script:
+        r.update_and_render(w, h, t)
+    import numpy as np
+    out = np.empty((h, w), dtype=np.uint32)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        r.update_and_render(w, h, hold, out)
+        frames += 1
+        el = time.perf_counter() - t0
+        if (el >= budget_s and frames >= 3) or frames >= 2000:
+            break
+    return frames / el, frames, el
+
+
+def load_traffic(workload_key):
+    """HBM bytes per fragment launch from the committed rocprofv3 --pmc summary (profiles/)."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload_key, {}).get('hbm_bytes_per_launch')
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit('--gpus N>1 needs torch.distributed.run with N processes')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('nccl', device_id=dev)
+
+    from swift3drenderer_amd import poses, scene
+    from swift3drenderer_amd.renderer import Renderer, band_row_ids
+
+    tmp = tempfile.mkdtemp(prefix=f's3r_bench_{rank}_')
+    data_path = os.path.join(tmp, f'{a.scene}.bin')
+    scene.write_named(a.scene, data_path)
+
+    W, H, B = a.width, a.height, a.band
+    N = world
+    script = poses.script(a.pose)
+    hold = poses.hold(a.pose)
+
+    r = Renderer(data_path, device=local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    rows = r.lib.s3r_band_rows_local(H, B, N, rank) if N > 1 else H
+    local_buf = torch.empty((max(rows, 1), W), dtype=torch.int32, device=dev)
+    if N > 1:
+        max_rows = max(r.lib.s3r_band_rows_local(H, B, N, p) for p in range(N))
+        send = torch.zeros((max_rows, W), dtype=torch.int32, device=dev)
+        recv = [torch.empty((max_rows, W), dtype=torch.int32, device=dev) for _ in range(N)] if rank == 0 else None
+        frame = torch.empty((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
+        ids = [torch.as_tensor(band_row_ids(H, B, N, p), device=dev) for p in range(N)]
+
+    def step(inp):
+        if N == 1:
+            r.render_bands(inp, W, H, H, 1, 0, local_buf.data_ptr(), sptr)
+            return
+        r.render_bands(inp, W, H, B, N, rank, send.data_ptr(), sptr)
+        dist.gather(send, recv, dst=0)
+        if rank == 0:
+            for p in range(N):
+                frame.index_copy_(0, ids[p], recv[p][: ids[p].numel()])
+
+    for t in script:                     # pose script (first call initialises), untimed
+        step(t)
+    for _ in range(a.warmup):
+        step(hold)
+    torch.cuda.synchronize(dev)
+
+    r.timing(True)
+    if N > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(hold)
+    torch.cuda.synchronize(dev)
+    if N > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    frag_ms, frame_ms, nfr = r.timing_collect()
+    r.timing(False)
+    if N > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    fps = a.steps / el
+    counts = r.scene_counts()      # V, I, A, texels, slots
+    nv, ni, na, ntex, nslots = counts[:5]
+    # algorithmic bytes of the fragment kernel per launch: this rank's framebuffer rows + the
+    # ripmap texels it may sample + the triangle setup records it reads
+    frag_bytes = 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
+    frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
+    achieved = frag_bytes / frag_avg_s / 1e9
+    workload = f'{a.scene}/{a.pose}/{W}x{H}/N{N}'
+
+    result = None
+    if rank == 0:
+        e2e = None
+        if not a.no_e2e and N == 1:
+            # updateAndRender into a caller-owned host buffer: includes the D2H over PCIe
+            host = np.empty((H, W), dtype=np.uint32)
+            r.configure(data_path, local)
+            for t in script:
+                r.update_and_render(W, H, t, host)
+            for _ in range(5):
+                r.update_and_render(W, H, hold, host)
+            n_e2e = max(20, min(200, a.steps))
+            t1 = time.perf_counter()
+            for _ in range(n_e2e):
+                r.update_and_render(W, H, hold, host)
+            e2e = n_e2e / (time.perf_counter() - t1)
+        cpu = None
+        if not a.no_cpu_baseline and N == 1:
+            cfps, cframes, cel = cpu_baseline(data_path, script, hold, W, H, a.cpu_seconds)
+            cpu = {'value': round(cfps, 4), 'unit': 'frames/s', 'cores': 1, 'kind': 'port',
+                   'sample': f'{cframes} frames of {a.scene}/{a.pose} at {W}x{H} in {cel:.1f} s, single thread, '
+                             f'oracle/render_oracle.c (gcc -O2) on {cpu_model()}'}
+        result = {
+            'metric': METRIC,
+            'value': round(fps, 3),
+            'unit': 'frames/s',
+            'n_gpus': N,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(el / a.steps * 1e3, 5),
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic: deterministic data.bin-format scene (SplitMix64 geometry, procedural ripmaps)',
+            'config': {'workload': f'updateAndRender frame, scene {a.scene} ({nslots // 2} triangles, '
+                                   f'{ntex >> 18} ripmap textures), pose {a.pose}, {W}x{H}',
+                       'scene': a.scene, 'pose': a.pose, 'width': W, 'height': H,
+                       'band_rows': B if N > 1 else H, 'parallelism': f'rows{N}' + ('+gather' if N > 1 else '')},
+            'mpixels_per_s': round(fps * W * H / 1e6, 2),
+            'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
+            'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
+            'e2e_fps_with_d2h': round(e2e, 3) if e2e else None,
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
+                         'kernel': 'k_fragment', 'algorithmic_bytes_per_launch': frag_bytes},
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(result), flush=True)
+    r.shutdown()
+    if N > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == '__main__':
+    main()

@@ -77,6 +77,9 @@ void s3r_scene_counts(uint64_t out[8]);
 /* Copy the current camera matrix (3 rows x 4) and raster factor. */
 void s3r_camera(float out_matrix[12], float *out_factor);
 
+/* Diagnostic counters of the S3R_STATS build (all zero in the product build). */
+void s3r_stats(uint64_t out[16], int reset);
+
 /* Self-test hooks (tests only): out[i] = the float32 value after n[i] sequential steps
  * s = fl(s + d) (the render.cpp:374/:378 walk) computed by the library's O(binades) walker;
  * lin[i]/del[i] = whether n[i] consecutive walk values are s + k*del exactly. */

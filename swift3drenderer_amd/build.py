@@ -35,28 +35,38 @@ def _newer(target: str, deps) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+STATS_LIB = os.path.join(PKG, 'librender_stats.so')
+
+
+def build_library(force: bool = False, verbose: bool = False, stats: bool = False, ablate: int = 0) -> str:
+    """stats=True builds the diagnostic variant (-DS3R_STATS, walker iteration counters) as
+    librender_stats.so; ablate=k builds a timing-only variant with parts of the fragment stage
+    removed (wrong pixels; tools/ablate.sh).  The product library has neither."""
+    tag = 'stats' if stats else (f'ablate{ablate}' if ablate else '')
+    bdir = os.path.join(BUILD, tag) if tag else BUILD
+    lib_path = os.path.join(BUILD, f'librender_{tag}.so') if ablate else (STATS_LIB if stats else LIB)
+    extra = (['-DS3R_STATS'] if stats else []) + ([f'-DS3R_ABLATE={ablate}'] if ablate else [])
+    os.makedirs(bdir, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith('.h')]
     headers.append(os.path.join(ROOT, 'include', 'render.h'))
     objs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + '.o')
+        o = os.path.join(bdir, src + '.o')
         objs.append(o)
         if force or not _newer(o, [s, *headers]):
-            cmd = [HIPCC, *FLAGS, '-x', 'hip', '-c', s, '-o', o]
+            cmd = [HIPCC, *FLAGS, *extra, '-x', 'hip', '-c', s, '-o', o]
             if verbose:
                 print(' '.join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)
-    if force or not _newer(LIB, objs):
-        cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', LIB, '-ldl']
+    if force or not _newer(lib_path, objs):
+        cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', lib_path, '-ldl']
         if verbose:
             print(' '.join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    if not _newer(DYLIB, [LIB]):
+    if not tag and not _newer(DYLIB, [LIB]):
         shutil.copyfile(LIB, DYLIB)
-    return LIB
+    return lib_path
 
 
 def build_data(force: bool = False) -> str:
@@ -68,6 +78,8 @@ def build_data(force: bool = False) -> str:
 
 def main():
     build_library(force='--force' in sys.argv, verbose=True)
+    if '--stats' in sys.argv:
+        build_library(force='--force' in sys.argv, verbose=True, stats=True)
     build_data()
     print(LIB)
 

@@ -225,20 +225,60 @@ __global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ cvb, c
     }
 }
 
-// ------------------------------------------------------------------ K4: fragment
-struct ChunkRec {           // 32 B, one per (triangle lane, chunk)
-    uint32_t k0;            // first pixel x of the triangle in this chunk, kInvalidK if none
-    uint32_t lin;           // bit c: component c is c + k*delta across the chunk
-    float c[3];             // exact barycentric value at x = k0
-    float del[3];
-};
-struct TriInfo {            // 32 B, one per triangle lane of the batch
-    float rvz[3];
-    uint32_t xmax;
-    float dx[3];
-    uint32_t slot;
-};
+#ifdef S3R_STATS
+__device__ unsigned long long g_stats[16];
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+#define S3R_IT(p) , (p)
+#else
+#define S3R_IT(p)
+#endif
 
+// ------------------------------------------------------------------ K3: row starts
+// rowtab[((slot * H + y) * (segs + 1) + j) * 4 + c], component c of the exact walk of row y
+// (render.cpp:374-379):  j = 0: at x = xmin, i.e. weight.wy after y - ymin steps of dy;
+// j = 1 + s: at x = s * segw, the first pixel of fragment segment s, for every segment boundary
+// inside (xmin, xmax].  One lane per (slot, row, component): one O(binades) walk along the row.
+__global__ void __launch_bounds__(192) k_rowstart(const TriSetup *__restrict__ tris, uint32_t H, uint32_t segs,
+                                                  uint32_t segw, float *__restrict__ rowtab) {
+    const uint32_t slot = blockIdx.x;
+    const uint32_t y = blockIdx.y * 64u + threadIdx.x;
+    const uint32_t c = threadIdx.y;
+    const TriSetup *t = tris + slot;
+    const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
+    if (h0.x == kDead) return;
+    const uint32_t ymax = reinterpret_cast<const uint4 *>(t)[1].x;
+    if (y < h0.w || y > ymax || y >= H) return;
+    float *dst = rowtab + ((size_t)slot * H + y) * (segs + 1) * 4 + c;
+    const float d = t->dx[c];
+#ifdef S3R_STATS
+    uint32_t it_row = 0, it_seg = 0;
+    float v = exact_walk(t->ws[c], t->dy[c], y - h0.w, &it_row);
+#else
+    float v = exact_walk(t->ws[c], t->dy[c], y - h0.w);
+#endif
+    dst[0] = v;
+    uint32_t kpos = h0.y;
+    for (uint32_t sg = h0.y / segw + 1u; sg < segs && sg * segw <= h0.z; sg++) {
+#ifdef S3R_STATS
+        v = exact_walk(v, d, sg * segw - kpos, &it_seg);
+#else
+        v = exact_walk(v, d, sg * segw - kpos);
+#endif
+        kpos = sg * segw;
+        dst[(1 + sg) * 4] = v;
+    }
+#ifdef S3R_STATS
+    atomicAdd(&g_stats[12], (unsigned long long)it_row);
+    atomicMax(&g_stats[13], (unsigned long long)it_row);
+    atomicAdd(&g_stats[14], (unsigned long long)it_seg);
+    atomicMax(&g_stats[15], (unsigned long long)it_seg);
+#endif
+}
+
+// ------------------------------------------------------------------ ripmap sample
 __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t base,
                                           float u, float v, float lvx, float lvy) {
     // getTextureColor, render.cpp:124-132
@@ -251,9 +291,113 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint
     return (base < ntex && ntex - base >= kTexTexels) ? tex[base + off] : 0u;
 }
 
+// ------------------------------------------------------------------ K4: fragment
+constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + component (63 lanes)
+constexpr uint32_t kWaves = 4;         // one wave per row: a workgroup is 4 consecutive local rows
+constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
+constexpr uint32_t kStateBatches = 4;  // batches whose walk state persists in LDS across chunks
+constexpr uint32_t kTables = 12;       // per wave: 64-entry exact-value tables for non-linear chunks
+
+struct Entry {                         // 48 B per listed triangle (LDS, shared by the 4 waves)
+    uint32_t slot, xmin, xmax, ymin;
+    uint32_t ymax;
+    float dx[3];
+    float rvz[3];
+    uint32_t pad;
+};
+
+struct FragShared {
+    Entry ent[kListMax];
+    uint32_t cnt, next;
+    float st_c[kWaves][kStateBatches * 64];
+    uint32_t st_k[kWaves][kStateBatches * 64];
+    float rc[kWaves][64], rd[kWaves][64];
+    uint32_t rt[kWaves][64];             // per (triangle, component) lane: table index, or kNoTable
+    uint32_t k0s[kWaves][kTPB + 3];
+    float tab[kWaves][kTables][64];      // exact S(c, d, k), k = 0..63, filled by sequential adds
+};
+constexpr uint32_t kNoTable = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask, uint32_t lane) {
+    return (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
+}
+
+// LDS hand-off between lanes of ONE wave: LDS operations of a wave execute in order, so only the
+// compiler must be kept from reordering across this point.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Out-of-line walker: one copy of the loop for every call site (code size, i-cache).
+__device__ __noinline__ float walk(float s, float d, uint32_t n
+#ifdef S3R_STATS
+                                   , uint32_t *iters
+#endif
+) {
+#ifdef S3R_STATS
+    return exact_walk(s, d, n, iters);
+#else
+    return exact_walk(s, d, n);
+#endif
+}
+
+
+// Wave 0 lists, in slot order, the live triangles whose bbox meets rows [y0, y1] and columns
+// [x0, x1], starting at slot `cursor`, at most kListMax; then all waves copy each listed triangle's
+// raster constants into LDS.  Must be reached by every wave of the workgroup.
+__device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, uint32_t y0, uint32_t y1,
+                           uint32_t x0, uint32_t x1, uint32_t cursor, FragShared &sh, uint32_t wave,
+                           uint32_t lane) {
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t cnt = 0;
+        while (cursor < nslots) {
+            const uint32_t s = cursor + lane;
+            bool act = false;
+            if (s < nslots) {
+                const uint4 h0 = reinterpret_cast<const uint4 *>(tris + s)[0];    // kind xmin xmax ymin
+                const uint32_t ymax = reinterpret_cast<const uint4 *>(tris + s)[1].x;
+                act = h0.x != kDead && h0.w <= y1 && ymax >= y0 && h0.y <= x1 && h0.z >= x0;
+            }
+            uint64_t mask = __ballot(act);
+            const uint32_t room = kListMax - cnt;
+            uint32_t pc = (uint32_t)__builtin_popcountll(mask);
+            uint32_t adv = 64;
+            if (pc > room) {
+                uint64_t rest = mask;
+                for (uint32_t i = 0; i < room; i++) rest &= rest - 1;
+                adv = (uint32_t)__builtin_ctzll(rest);          // first slot that does not fit
+                mask ^= rest;
+                pc = room;
+            }
+            if (act && ((mask >> lane) & 1ull)) sh.ent[cnt + lane_prefix(mask, lane)].slot = s;
+            cnt += pc;
+            cursor += adv;
+            if (cnt == kListMax) break;
+        }
+        if (lane == 0) { sh.cnt = cnt; sh.next = cursor < nslots ? cursor : nslots; }
+    }
+    __syncthreads();
+    const uint32_t cnt = sh.cnt;
+    for (uint32_t i = wave * 64 + lane; i < cnt; i += kWaves * 64) {
+        const TriSetup *t = tris + sh.ent[i].slot;
+        const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
+        const uint4 h1 = reinterpret_cast<const uint4 *>(t)[1];
+        const float4 dx = reinterpret_cast<const float4 *>(t)[3];
+        const float4 rz = reinterpret_cast<const float4 *>(t)[5];
+        Entry &e = sh.ent[i];
+        e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
+        e.dx[0] = dx.x; e.dx[1] = dx.y; e.dx[2] = dx.z;
+        e.rvz[0] = rz.x; e.rvz[1] = rz.y; e.rvz[2] = rz.z;
+    }
+    __syncthreads();
+}
+
 // Deferred shading of the winning triangle (render.cpp:366-371).
-__device__ uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
-                          const uint32_t *__restrict__ tex, uint32_t ntex) {
+__device__ __noinline__ uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
+                                       const uint32_t *__restrict__ tex, uint32_t ntex) {
     const float4 *q = reinterpret_cast<const float4 *>(tp);
     const uint4 hdr = reinterpret_cast<const uint4 *>(tp)[0];
     const uint4 hdr2 = reinterpret_cast<const uint4 *>(tp)[1];
@@ -287,117 +431,205 @@ __device__ uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, f
     return rgb_pack(s * col.x, s * col.y, s * col.z);
 }
 
-template <int NCH>
-__global__ void __launch_bounds__(64) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
-                                                 const uint32_t *__restrict__ tex, uint32_t ntex,
-                                                 uint32_t *__restrict__ out, uint32_t W, uint32_t H,
-                                                 uint32_t band, uint32_t nparts, uint32_t part,
-                                                 uint32_t segs) {
-    __shared__ ChunkRec rec[64];
-    __shared__ TriInfo info[64];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t lr = blockIdx.x / segs, seg = blockIdx.x - lr * segs;
-    const uint32_t y = ((lr / band) * nparts + part) * band + lr % band;   // interleaved row bands
-    if (y >= H) return;
-    const uint32_t xs = seg * 64u * NCH;
-    const uint32_t xe = min(W, xs + 64u * NCH) - 1u;
+// A workgroup = 4 waves = 4 consecutive local rows x one segment of SEGCH 64-pixel chunks.  The
+// triangles meeting that block are listed once in LDS (slot order).  For each chunk, each wave takes
+// them kTPB at a time: its lanes first act as (triangle, barycentric component) pairs and advance
+// that component's exact walk (render.cpp:374) to the chunk, publishing (value, step) in LDS; then
+// its lanes act as pixels: edge test, 1/z, strict '>' depth test in registers; the winner is shaded.
+template <uint32_t SEGCH>
+__global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
+                                                  const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
+                                                  uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
+                                                  uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
+                                                  uint32_t rows_local) {
+    __shared__ FragShared sh;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t blk = blockIdx.x / segs, seg = blockIdx.x - blk * segs;
+    auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
+    const uint32_t lr0 = blk * kWaves;
+    const uint32_t lr = lr0 + wave;
+    const uint32_t y = row_of(lr);
+    const bool row_ok = lr < rows_local && y < H;
+    uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
+    for (uint32_t k = 0; k < kWaves && lr0 + k < rows_local; k++) {
+        const uint32_t yy = row_of(lr0 + k);
+        y0 = min(y0, yy); y1 = max(y1, yy);
+    }
+    const uint32_t xs = seg * 64u * SEGCH;
+    const uint32_t xe = min(W, xs + 64u * SEGCH) - 1u;
+    const uint32_t tl = lane / 3u, comp = lane - 3u * tl;                  // (triangle, component) role
+    float *st_c = sh.st_c[wave];
+    uint32_t *st_k = sh.st_k[wave];
+    float *rc = sh.rc[wave], *rd = sh.rd[wave];
+    uint32_t *k0s = sh.k0s[wave];
+#ifdef S3R_STATS
+    uint32_t st_row = 0, st_chunk = 0, st_pix = 0, st_irr = 0, st_tests = 0, st_batches = 0;
+    uint32_t *p_chunk = &st_chunk, *p_pix = &st_pix;
+#endif
 
-    float depth[NCH], bw0[NCH], bw1[NCH], bw2[NCH];
-    int win[NCH];
-#pragma unroll
-    for (int q = 0; q < NCH; q++) { depth[q] = 0.0f; win[q] = -1; bw0[q] = bw1[q] = bw2[q] = 0.0f; }
-
-    for (uint32_t base = 0; base < nslots; base += 64u) {
-        // ---- lanes as triangles
-        const uint32_t s = base + lane;
-        bool act = false;
-        uint4 h0 = make_uint4(0, 0, 0, 0);
-        uint32_t ymax = 0;
-        if (s < nslots) {
-            h0 = reinterpret_cast<const uint4 *>(tris + s)[0];
-            ymax = reinterpret_cast<const uint4 *>(tris + s)[1].x;
-            act = h0.x != kDead && y >= h0.w && y <= ymax && h0.y <= xe && h0.z >= xs;
-        }
-        const uint64_t mask = __ballot(act);
-        if (mask == 0) continue;
-        float c0 = 0, c1 = 0, c2 = 0, dx0 = 0, dx1 = 0, dx2 = 0;
-        uint32_t kpos = 0;
-        if (act) {
-            const float4 *q = reinterpret_cast<const float4 *>(tris + s);
-            const float4 ws = q[2], dx = q[3], dy = q[4], rz = q[5];
-            const uint32_t j = y - h0.w;
-            c0 = exact_walk(ws.x, dy.x, j);          // row start wy after j steps (render.cpp:378)
-            c1 = exact_walk(ws.y, dy.y, j);
-            c2 = exact_walk(ws.z, dy.z, j);
-            dx0 = dx.x; dx1 = dx.y; dx2 = dx.z;
-            kpos = h0.y;
-            TriInfo ti;
-            ti.rvz[0] = rz.x; ti.rvz[1] = rz.y; ti.rvz[2] = rz.z; ti.xmax = h0.z;
-            ti.dx[0] = dx.x; ti.dx[1] = dx.y; ti.dx[2] = dx.z; ti.slot = s;
-            info[lane] = ti;
-        }
-#pragma unroll
-        for (int q = 0; q < NCH; q++) {
-            const uint32_t cx0 = xs + 64u * q;
-            if (cx0 > xe) break;
-            const uint32_t cx1 = min(cx0 + 63u, xe);
-            if (act) {
-                ChunkRec r;
-                r.k0 = kInvalidK;
-                r.lin = 0;
-                r.c[0] = r.c[1] = r.c[2] = 0.0f;
-                r.del[0] = r.del[1] = r.del[2] = 0.0f;
-                if (h0.y <= cx1 && h0.z >= cx0) {
-                    const uint32_t k0 = max(cx0, h0.y);
-                    const uint32_t m = min(cx1, h0.z) - k0 + 1u;
-                    c0 = exact_walk(c0, dx0, k0 - kpos);    // pixel walk (render.cpp:374)
-                    c1 = exact_walk(c1, dx1, k0 - kpos);
-                    c2 = exact_walk(c2, dx2, k0 - kpos);
-                    kpos = k0;
-                    r.k0 = k0;
-                    r.c[0] = c0; r.c[1] = c1; r.c[2] = c2;
-                    r.lin = (chunk_linear(c0, dx0, m, &r.del[0]) ? 1u : 0u) |
-                            (chunk_linear(c1, dx1, m, &r.del[1]) ? 2u : 0u) |
-                            (chunk_linear(c2, dx2, m, &r.del[2]) ? 4u : 0u);
+    build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
+    const uint32_t n0 = sh.cnt;
+    const bool overflow = sh.next < nslots;   // > kListMax triangles: stateless rounds per chunk
+    if (!overflow && row_ok) {
+        // walk state of the first batches: the exact row start (rowtab) at x = xmin
+        for (uint32_t b = 0; b < kStateBatches && b * kTPB < n0; b++) {
+            const uint32_t idx = b * kTPB + tl;
+            if (lane < 63 && idx < n0) {
+                const Entry &e = sh.ent[idx];
+                if (y >= e.ymin && y <= e.ymax) {
+                    // exact value AT this triangle's first pixel in the segment (xmin, or the
+                    // segment start): the first chunk then needs no walking at all
+                    const bool inside = e.xmin >= xs;
+                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * H + y) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
+                    st_k[b * 64 + lane] = inside ? e.xmin : xs;
                 }
-                rec[lane] = r;
             }
-            __syncthreads();
-            // ---- lanes as pixels
-            const uint32_t x = cx0 + lane;
-            uint64_t mm = mask;
-            while (mm) {
-                const uint32_t t = (uint32_t)__builtin_ctzll(mm);
-                mm &= mm - 1;
-                const ChunkRec r = rec[t];
-                if (r.k0 == kInvalidK) continue;
-                const TriInfo ti = info[t];
-                if (x >= r.k0 && x <= ti.xmax) {
-                    const uint32_t off = x - r.k0;
+        }
+        wave_sync();
+    }
+
+    uint32_t *row = out + (size_t)lr * W;
+    for (uint32_t q = 0; q < SEGCH; q++) {
+        const uint32_t cx0 = xs + 64u * q;
+        if (cx0 > xe) break;
+        const uint32_t cx1 = min(cx0 + 63u, xe);
+        const uint32_t x = cx0 + lane;
+        float depth = 0.0f, bw0 = 0.0f, bw1 = 0.0f, bw2 = 0.0f;
+        int win = -1;
+
+        uint32_t cursor = 0, cnt = n0;
+        for (;;) {
+            if (overflow) {
+                build_list(tris, nslots, y0, y1, cx0, cx1, cursor, sh, wave, lane);
+                cnt = sh.cnt;
+                cursor = sh.next;
+            }
+            for (uint32_t b = 0; row_ok && b * kTPB < cnt; b++) {
+                const bool stateful = !overflow && b < kStateBatches;
+                // ---- lanes as (triangle, component): advance the exact walk to this chunk
+                const uint32_t idx = b * kTPB + tl;
+                bool ov = false, lin = false, neg = false;
+                float c = 0.0f, d = 0.0f, del = 0.0f;
+                uint32_t k0 = 0, m = 0;
+                if (lane < 63 && idx < cnt) {
+                    const Entry &e = sh.ent[idx];
+                    ov = y >= e.ymin && y <= e.ymax && e.xmin <= cx1 && e.xmax >= cx0;
+                    if (ov) {
+                        d = e.dx[comp];
+                        k0 = max(cx0, e.xmin);
+                        m = min(cx1, e.xmax) - k0 + 1u;
+                        if (stateful) {
+                            // state = exact value at pixel kp (the segment start / xmin, or the last
+                            // pixel of the previous chunk); contiguous chunks need 0 or 1 step
+                            const uint32_t kp = st_k[b * 64 + lane];
+                            const float cp = st_c[b * 64 + lane];
+                            c = k0 == kp ? cp : (k0 == kp + 1u ? cp + d : walk(cp, d, k0 - kp S3R_IT(p_chunk)));
+                        } else {
+                            const bool inside = e.xmin >= xs;
+                            const float c0v = rowtab[(((size_t)e.slot * H + y) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
+                            c = walk(c0v, d, k0 - (inside ? e.xmin : xs) S3R_IT(p_chunk));
+                        }
+                        lin = chunk_linear(c, d, m, &del);
+                        if (lin) neg = c < 0.0f && c + (float)(m - 1u) * del < 0.0f;   // monotone walk
+                        if (comp == 0) k0s[tl] = k0;
+                    }
+                }
+                const uint64_t ovm = __ballot(ov && comp == 0);
+                if (ovm == 0) continue;
+                // a triangle with one component negative over the whole chunk covers none of it
+                uint64_t negm = __ballot(neg);
+                const uint64_t irrm = __ballot(ov && !lin && !((negm >> (3u * tl)) & 7ull));
+                uint32_t tix = kNoTable;
+                float last = c + (float)(m - 1u) * del;
+                if (ov && !lin) {
+                    if ((negm >> (3u * tl)) & 7ull) {
+                        last = c;                       // pruned: keep the state at the chunk start
+                        m = 1u;
+                    } else {
+                        const uint32_t r = lane_prefix(irrm, lane);
+                        if (r < kTables) {
+                            // the reference's own loop: m - 1 sequential float adds (render.cpp:374)
+                            float v = c;
+                            float *tb = sh.tab[wave][r];
+                            tb[0] = v;
+                            for (uint32_t k = 1; k < m; k++) { v = v + d; tb[k] = v; }
+                            last = v;
+                            tix = r;
+                        } else {
+                            last = walk(c, d, m - 1u S3R_IT(p_chunk));
+                        }
+                        neg = c < 0.0f && last < 0.0f;
+                    }
+                }
+                negm = __ballot(neg);
+                if (ov) {
+                    rc[lane] = c;
+                    rd[lane] = del;
+                    sh.rt[wave][lane] = tix;
+                    if (stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = k0 + m - 1u; }
+                }
+                wave_sync();
+#ifdef S3R_STATS
+                st_batches++;
+                st_irr += (ov && !lin) ? 1u : 0u;
+#endif
+                // ---- lanes as pixels: triangles in slot order (bit 3t of `live`)
+                const uint64_t neg3 = negm | (negm >> 1) | (negm >> 2);
+                uint64_t live = ovm & ~neg3 & 0x9249249249249249ull;   // bits 0, 3, 6, ...
+                while (live) {
+                    const uint32_t t = (uint32_t)__builtin_ctzll(live) / 3u;
+                    live &= live - 1;
+                    const Entry &e = sh.ent[b * kTPB + t];
+                    const uint32_t tk0 = k0s[t];
+                    if (x < tk0 || x > e.xmax) continue;
+#ifdef S3R_STATS
+                    st_tests++;
+#endif
+                    const uint32_t off = x - tk0;
                     const float fo = (float)off;
-                    const float a0 = (r.lin & 1u) ? r.c[0] + fo * r.del[0] : exact_walk(r.c[0], ti.dx[0], off);
-                    const float a1 = (r.lin & 2u) ? r.c[1] + fo * r.del[1] : exact_walk(r.c[1], ti.dx[1], off);
-                    const float a2 = (r.lin & 4u) ? r.c[2] + fo * r.del[2] : exact_walk(r.c[2], ti.dx[2], off);
-                    if (a0 >= 0 && a1 >= 0 && a2 >= 0) {                         // :362
-                        const float ooz = (ti.rvz[0] * a0 + ti.rvz[1] * a1) + ti.rvz[2] * a2;   // :363
-                        if (ooz > depth[q]) {                                        // :364
-                            depth[q] = ooz; win[q] = (int)ti.slot;
-                            bw0[q] = a0; bw1[q] = a1; bw2[q] = a2;
+                    float a[3];
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++) {
+                        const uint32_t l = 3u * t + cc;
+                        const uint32_t ti = sh.rt[wave][l];
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
+                        a[cc] = rc[l] + fo * rd[l];
+#else
+                        if (ti == kNoTable && !((irrm >> l) & 1ull))
+                            a[cc] = rc[l] + fo * rd[l];
+                        else if (ti != kNoTable)
+                            a[cc] = sh.tab[wave][ti][off];
+                        else
+                            a[cc] = walk(rc[l], e.dx[cc], off S3R_IT(p_pix));
+#endif
+                    }
+                    if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                                  // :362
+                        const float ooz = (e.rvz[0] * a[0] + e.rvz[1] * a[1]) + e.rvz[2] * a[2]; // :363
+                        if (ooz > depth) {                                                         // :364
+                            depth = ooz; win = (int)e.slot; bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
                         }
                     }
                 }
+                wave_sync();
             }
-            __syncthreads();
+            if (!overflow || cursor >= nslots) break;
+        }
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 1)
+        if (row_ok && x <= xe) row[x] = win < 0 ? kBackground : (uint32_t)win ^ __float_as_uint(bw0 + bw1 + bw2 + depth);
+#else
+        if (row_ok && x <= xe) row[x] = win < 0 ? kBackground : shade(tris + win, bw0, bw1, bw2, depth, tex, ntex);
+#endif
+    }
+#ifdef S3R_STATS
+    {
+        const uint32_t vals[6] = {st_row, st_chunk, st_pix, st_irr, st_tests, st_batches};
+        for (int k = 0; k < 6; k++) {
+            uint32_t v = vals[k], m = wave_max(v);
+            for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+            if (lane == 0) { atomicAdd(&g_stats[2 * k], (unsigned long long)v); atomicAdd(&g_stats[2 * k + 1], (unsigned long long)m); }
         }
     }
-    uint32_t *row = out + (size_t)lr * W;
-#pragma unroll
-    for (int q = 0; q < NCH; q++) {
-        const uint32_t x = xs + 64u * q + lane;
-        if (x <= xe) {
-            row[x] = win[q] < 0 ? kBackground : shade(tris + win[q], bw0[q], bw1[q], bw2[q], depth[q], tex, ntex);
-        }
-    }
+#endif
 }
 
 // ------------------------------------------------------------------ self-test kernel
@@ -418,8 +650,22 @@ void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *
     hipLaunchKernelGGL(k_walk_test, dim3((count + 255) / 256), dim3(256), 0, st, s, d, n, out, lin, del, count);
 }
 
+void stats_read(unsigned long long out[16], bool reset) {
+#ifdef S3R_STATS
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(unsigned long long) * 16, 0, hipMemcpyDeviceToHost);
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z, 0, hipMemcpyHostToDevice);
+    }
+#else
+    (void)reset;
+    for (int i = 0; i < 16; i++) out[i] = 0;
+#endif
+}
+
 // ------------------------------------------------------------------ launchers
-constexpr int kNCH = 8;
+constexpr uint32_t kSegChunks = 16;   // 1024-pixel segments
 
 void launch_vertex(const float4 *vtx, uint32_t nv, const float4 *nrm, uint32_t na, const Mat34 &m,
                    float factor, float sw, float sh, float4 *cv, float4 *rv, float4 *ncam, hipStream_t st) {
@@ -439,16 +685,24 @@ void launch_setup(const float4 *cv, const float4 *rv, const float4 *ncam, const 
                        aidx, ntri, factor, sw, sh, tris);
 }
 
-uint32_t fragment_segment_pixels() { return 64u * kNCH; }
+uint32_t fragment_segment_pixels() { return 64u * kSegChunks; }
 
-void launch_fragment(const TriSetup *tris, uint32_t nslots, const uint32_t *tex, uint32_t ntex, uint32_t *out,
-                     uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     hipStream_t st) {
-    const uint32_t segs = (W + 64u * kNCH - 1) / (64u * kNCH);
-    const uint64_t blocks = (uint64_t)rows_local * segs;
+uint32_t fragment_segments(uint32_t W) { return (W + 64u * kSegChunks - 1) / (64u * kSegChunks); }
+
+void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st) {
+    if (nslots == 0 || H == 0) return;
+    hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, fragment_segments(W),
+                       64u * kSegChunks, rowtab);
+}
+
+void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
+                     uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+                     uint32_t rows_local, hipStream_t st) {
+    const uint32_t segs = (W + 64u * kSegChunks - 1) / (64u * kSegChunks);
+    const uint64_t blocks = (uint64_t)((rows_local + kWaves - 1) / kWaves) * segs;
     if (blocks == 0) return;
-    hipLaunchKernelGGL(k_fragment<kNCH>, dim3((uint32_t)blocks), dim3(64), 0, st, tris, nslots, tex, ntex, out,
-                       W, H, band, nparts, part, segs);
+    hipLaunchKernelGGL(k_fragment<kSegChunks>, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab,
+                       tex, ntex, out, W, H, band, nparts, part, segs, rows_local);
 }
 
 }  // namespace s3r

@@ -60,6 +60,8 @@ struct Lib {
     TriSetup *tris = nullptr;
     uint32_t *frame = nullptr;
     size_t frame_cap = 0;
+    float *rowtab = nullptr;       // 2T x H x float4 exact row starts
+    size_t rowtab_cap = 0;
     hipStream_t stream = nullptr;
 
     // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
@@ -231,7 +233,8 @@ void release_all() {
         (void)hipSetDevice(g.device);
         if (g.stream) (void)hipStreamSynchronize(g.stream);
         unregister_all();
-        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.cv, g.rv, g.ncam, g.tris, g.frame};
+        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.cv, g.rv, g.ncam, g.tris, g.frame,
+                        g.rowtab};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
         for (auto &t : g.tslots) {
@@ -282,8 +285,16 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     const float sw = (float)W, sh = (float)H;
     launch_vertex(g.vtx, g.nv, g.nrm, g.na, g.m, g.factor, sw, sh, g.cv, g.rv, g.ncam, st);
     launch_setup(g.cv, g.rv, g.ncam, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.factor, sw, sh, g.tris, st);
+    const size_t need = (size_t)2 * g.ntri * H * (fragment_segments(W) + 1) * 4;
+    if (g.rowtab_cap < need) {
+        HIPCHECK(hipStreamSynchronize(st));
+        if (g.rowtab) HIPCHECK(hipFree(g.rowtab));
+        g.rowtab = dalloc<float>(need);
+        g.rowtab_cap = need;
+    }
+    launch_rowstart(g.tris, 2 * g.ntri, W, H, g.rowtab, st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_fragment(g.tris, 2 * g.ntri, g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
+    launch_fragment(g.tris, 2 * g.ntri, g.rowtab, g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipGetLastError());
 }
@@ -384,6 +395,15 @@ __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
 __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {
     memcpy(out_matrix, g.m.m, sizeof g.m.m);
     if (out_factor) *out_factor = g.factor;
+}
+
+// Diagnostic counters (non-zero only in the S3R_STATS build, librender_stats.so): pairs of
+// (sum over lanes, sum over waves of the wave maximum) for row-walk, chunk-walk and per-pixel walker
+// iterations, irregular chunk components, pixel-triangle tests and triangle batches.
+__attribute__((visibility("default"))) void s3r_stats(uint64_t out[16], int reset) {
+    unsigned long long tmp[16];
+    stats_read(tmp, reset != 0);
+    for (int i = 0; i < 16; i++) out[i] = tmp[i];
 }
 
 // ---- self-test hooks: the exact repeated-addition walker on the host and on the device ----

@@ -54,21 +54,43 @@ S3R_HD float quot_approx(float num, float den) {
 #endif
 }
 
+// Regular steps available from s inside its binade [2^(e-127), 2^(e-126)) with steady step delta:
+// the number of j >= 0 whose input s_j = s + j*delta still rounds on this binade's grid u, i.e.
+// |s_j| + |d| < 2^(e-126) moving away from zero, |s_j| - |d| >= 2^(e-127) moving towards it.  In
+// units of u every quantity is an integer below 2^24 (|d| need not be), so floats hold them exactly:
+// with A = |delta|/u, D = |d|/u, the bound on j*A is N = T - floor(D) - 1 (away; T = edge distance)
+// or N = L - ceil(D) (towards; L = distance to the lower edge); the count is floor(N/A) + 1.
+S3R_HD float regular_steps(float s, float d, float delta, uint32_t e) {
+    const float inv_u = pow2_biased(277u - e);          // 1/u = 2^(150 - e): biased exponent 277 - e
+    const float as = fabsf(s);
+    const float A = fabsf(delta) * inv_u;
+    const float D = fabsf(d) * inv_u;
+    const bool away = (s > 0.0f) == (delta > 0.0f);
+    const float N = away ? (pow2_biased(e + 1u) - as) * inv_u - floorf(D) - 1.0f
+                         : (as - pow2_biased(e)) * inv_u - ceilf(D);
+    if (N < 0.0f) return 0.0f;
+    float q = floorf(quot_approx(N, A));                  // ~1 ulp; corrected exactly below
+    if (q * A > N) q -= 1.0f;
+    if (q * A > N) q -= 1.0f;
+    if ((q + 1.0f) * A <= N) q += 1.0f;
+    return q + 1.0f;
+}
+
 // exact_walk(s, d, n) == the float32 value after n sequential steps s = fl(s + d)
 // (render.cpp:374 `weight.w += weight.dx`, :378 `weight.wy += weight.dy`), in O(binades) work.
 //
-// Inside one binade [2^e, 2^(e+1)) every sum s + d rounds onto the grid u = 2^(e-23), and the step
-// fl(s + d) - s is the same for every s there (for a d exactly half-way between grid points the
-// tie-to-even parity settles after at most one step).  So once two consecutive steps are equal and
-// stay in the binade, j more steps are s + j*delta, exactly representable, as long as the last
-// sum stays 2 steps clear of the binade edge.  Near zero (|s| < 4|d|, or < 8|d| heading towards
-// zero) and at binade edges we take single steps.  Validated against the sequential loop
-// (tests/test_exact_walk.py).
-S3R_HD float exact_walk(float s, float d, uint32_t n) {
+// Inside one binade every sum s + d rounds onto the grid u, and the step fl(s + d) - s is the same
+// for every s there (for a d exactly half-way between grid points the tie-to-even parity settles
+// after at most one step).  Once two consecutive steps are equal and in the binade, all
+// regular_steps() steps up to the binade edge are s + j*delta (exact), then one ordinary add crosses
+// the edge.  Near zero (|s| < 4|d|, or < 8|d| heading towards zero) we take single steps.
+// Validated against the sequential loop (tests/test_exact_walk.py).
+S3R_HD float exact_walk(float s, float d, uint32_t n, uint32_t *iters = nullptr) {
     if (n == 0) return s;
     const float ad = fabsf(d);
     if (ad == 0.0f || !is_finite(s) || !is_finite(d)) return s + d;   // one add is a fixed point
     while (n) {
+        if (iters) ++*iters;
         const float as = fabsf(s);
         const bool towards_zero = (s < 0.0f) != (d < 0.0f);
         if (!(as >= 4.0f * ad) || (towards_zero && as < 8.0f * ad)) { s = s + d; --n; continue; }
@@ -76,22 +98,16 @@ S3R_HD float exact_walk(float s, float d, uint32_t n) {
         if (n == 1) return s1;
         const float s2 = s1 + d;
         const uint32_t e = fexp(s);
-        if (e == 0u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - s) != (s2 - s1)) {
+        if (e < 32u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - s) != (s2 - s1)) {
             s = s1; --n; continue;
         }
         const float delta = s1 - s;           // exact (same binade)
         if (delta == 0.0f) return s;          // fl(s + d) == s: stagnated for good
-        const float adel = fabsf(delta);
-        const bool away = (s > 0.0f) == (delta > 0.0f);
-        const float room = away ? pow2_biased(e + 1) - as : as - pow2_biased(e);   // exact (Sterbenz)
-        const float q = quot_approx(room, adel);
-        uint32_t j = q >= 3.0f ? (uint32_t)q - 2u : 0u;
-        // valid iff (j + 2) * |delta| <= room; the product is exact whenever it is <= room
-        while (j > 0u && (float)(j + 2u) * adel > room) --j;
-        if (j < 2u) { s = s1; --n; continue; }
-        if (j > n) j = n;
-        s = s + (float)j * delta;             // exact: lands on the grid inside the binade
-        n -= j;
+        float j = regular_steps(s, d, delta, e);
+        if (j < 2.0f) { s = s1; --n; continue; }
+        if (j > (float)n) j = (float)n;
+        s = s + j * delta;                    // exact: lands on the grid, at most on the edge
+        n -= (uint32_t)j;
     }
     return s;
 }
@@ -109,14 +125,11 @@ S3R_HD bool chunk_linear(float c, float d, uint32_t m, float *delta) {
     if (!(ac >= 4.0f * ad) || (towards_zero && ac < 8.0f * ad)) return false;
     const float s1 = c + d, s2 = s1 + d;
     const uint32_t e = fexp(c);
-    if (e == 0u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - c) != (s2 - s1)) return false;
+    if (e < 32u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - c) != (s2 - s1)) return false;
     const float del = s1 - c;
     *delta = del;
     if (del == 0.0f) return true;
-    const float adel = fabsf(del);
-    const bool away = (c > 0.0f) == (del > 0.0f);
-    const float room = away ? pow2_biased(e + 1) - ac : ac - pow2_biased(e);
-    return (float)(m + 1u) * adel <= room;                // jump of m-1 steps is valid
+    return regular_steps(c, d, del, e) >= (float)(m - 1u);   // m-1 regular steps reach the chunk end
 }
 
 // ---- float3 helpers in the reference's evaluation order ----

@@ -14,11 +14,18 @@ void launch_setup(const float4 *cv, const float4 *rv, const float4 *ncam, const 
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
 // out[lr * W + x].
-void launch_fragment(const TriSetup *tris, uint32_t nslots, const uint32_t *tex, uint32_t ntex, uint32_t *out,
-                     uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     hipStream_t st);
+void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
+                     uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+                     uint32_t rows_local, hipStream_t st);
+
+// rowtab (nslots x H x (segments + 1) x float4): exact barycentrics of every live slot's bbox rows at
+// x = xmin and at each fragment-segment boundary inside the bbox.
+void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st);
+uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
+
+void stats_read(unsigned long long out[16], bool reset);
 
 void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,
                       uint32_t count, hipStream_t st);

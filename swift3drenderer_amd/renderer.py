@@ -14,7 +14,7 @@ import numpy as np
 from .abi import Input, pixel_data_for
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, 'librender.so')
+LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 
 EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_render_bands', 's3r_band_rows_local',
            's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
