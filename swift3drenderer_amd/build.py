@@ -38,6 +38,21 @@ def _newer(target: str, deps) -> bool:
 STATS_LIB = os.path.join(PKG, 'librender_stats.so')
 
 
+def build_variant(tag: str, defines: dict, verbose: bool = False) -> str:
+    """A tuning variant (build/librender_<tag>.so) with extra -D knobs; tools/variants.sh."""
+    bdir = os.path.join(BUILD, tag)
+    os.makedirs(bdir, exist_ok=True)
+    lib_path = os.path.join(BUILD, f'librender_{tag}.so')
+    extra = [f'-D{k}={v}' for k, v in defines.items()]
+    objs = []
+    for src in SOURCES:
+        o = os.path.join(bdir, src + '.o')
+        subprocess.run([HIPCC, *FLAGS, *extra, '-x', 'hip', '-c', os.path.join(CSRC, src), '-o', o], check=True)
+        objs.append(o)
+    subprocess.run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', lib_path, '-ldl'], check=True)
+    return lib_path
+
+
 def build_library(force: bool = False, verbose: bool = False, stats: bool = False, ablate: int = 0) -> str:
     """stats=True builds the diagnostic variant (-DS3R_STATS, walker iteration counters) as
     librender_stats.so; ablate=k builds a timing-only variant with parts of the fragment stage

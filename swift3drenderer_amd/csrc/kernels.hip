@@ -1,9 +1,9 @@
 // kernels.hip -- the gfx950 HIP kernels of the rasterizer.
 //
-//   k_vertex    render.cpp:284-292  camera-space + raster transform of the vertex stream and the
-//                                   normal transform of the attribute stream (coalesced float4).
-//   k_setup     render.cpp:297-359  per triangle: gather, reject, near-plane clip (:212-262), cull,
-//                                   raster setup.  Writes slot t and, for a clip split, slot T+t.
+//   k_setup     render.cpp:284-359  per triangle: vertex + normal transform of its corners, gather,
+//                                   reject, near-plane clip (:212-262), cull, raster setup.  Writes
+//                                   slot t and, for a clip split, slot T+t.
+//   k_rowstart  render.cpp:374-379  exact row-start / segment-start barycentrics per (slot, row).
 //   k_fragment  render.cpp:360-382  one wave per (row, 64*NCH-pixel segment).  Triangles are taken
 //                                   in slot order, 64 at a time: lanes first act as TRIANGLES and
 //                                   walk each triangle's exact barycentric sequence to this row
@@ -21,34 +21,12 @@
 
 namespace s3r {
 
-// ------------------------------------------------------------------ K1: vertex + normal transform
+// ------------------------------------------------------------------ transforms
 // simd_mul(simd_float4x3, simd_float4) = ((c0*x + c1*y) + c2*z) + c3*w
 __device__ __forceinline__ F3 mat_mul(const Mat34 &m, float4 v) {
     return mk3(((m.m[0][0] * v.x + m.m[0][1] * v.y) + m.m[0][2] * v.z) + m.m[0][3] * v.w,
                ((m.m[1][0] * v.x + m.m[1][1] * v.y) + m.m[1][2] * v.z) + m.m[1][3] * v.w,
                ((m.m[2][0] * v.x + m.m[2][1] * v.y) + m.m[2][2] * v.z) + m.m[2][3] * v.w);
-}
-
-__global__ void __launch_bounds__(256) k_vertex(const float4 *__restrict__ vtx, uint32_t nv,
-                                                const float4 *__restrict__ nrm, uint32_t na, Mat34 m,
-                                                float factor, float half_w, float half_h,
-                                                float4 *__restrict__ cv, float4 *__restrict__ rv,
-                                                float4 *__restrict__ ncam) {
-    const uint32_t n = nv > na ? nv : na;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        if (i < nv) {
-            const F3 c = mat_mul(m, vtx[i]);
-            const float nz = -c.z;
-            cv[i] = make_float4(c.x, c.y, c.z, 0.0f);
-            // (cv.x, -cv.y, 0) * factor / -cv.z + (W/2, H/2, -cv.z)   (render.cpp:288)
-            rv[i] = make_float4((c.x * factor) / nz + half_w, ((-c.y) * factor) / nz + half_h,
-                                (0.0f * factor) / nz + nz, 0.0f);
-        }
-        if (i < na) {
-            const F3 r = mat_mul(m, nrm[i]);                       // render.cpp:291
-            ncam[i] = make_float4(r.x, r.y, r.z, 0.0f);
-        }
-    }
 }
 
 // ------------------------------------------------------------------ K2: gather / clip / cull / setup
@@ -187,21 +165,27 @@ __device__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, Tr
     *out = t;
 }
 
-__global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ cvb, const float4 *__restrict__ rvb,
-                                               const float4 *__restrict__ ncam, const float4 *__restrict__ pay,
-                                               const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx,
-                                               const uint32_t *__restrict__ aidx, uint32_t ntri, float factor,
-                                               float sw, float sh, TriSetup *__restrict__ tris) {
+// One thread per original triangle; the vertex and normal transforms of its three corners
+// (render.cpp:285-292) are done in place, so the frame needs no camera-space vertex arrays (each
+// corner reads 16 + 16 B instead of writing and re-reading 48 B of transformed data).
+__global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ vtx, const float4 *__restrict__ nrm,
+                                               const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
+                                               const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
+                                               uint32_t ntri, Mat34 m, float factor, float sw, float sh,
+                                               TriSetup *__restrict__ tris) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntri) return;
+    const float half_w = sw / 2, half_h = sh / 2;
     Vert d[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const uint32_t vi = vidx[3 * t + k], ai = aidx[3 * t + k];
-        const float4 c = cvb[vi], r = rvb[vi], n = ncam[ai];
-        d[k].cv = mk3(c.x, c.y, c.z);
-        d[k].rv = mk3(r.x, r.y, r.z);
-        d[k].n = mk3(n.x, n.y, n.z);
+        const F3 c = mat_mul(m, vtx[vi]);                                  // :286
+        const float nz = -c.z;
+        d[k].cv = c;
+        // (cv.x, -cv.y, 0) * factor / -cv.z + (W/2, H/2, -cv.z)            // :288
+        d[k].rv = mk3((c.x * factor) / nz + half_w, ((-c.y) * factor) / nz + half_h, (0.0f * factor) / nz + nz);
+        d[k].n = mat_mul(m, nrm[ai]);                                       // :291
         d[k].pay = pay[ai];
     }
     const bool textured = disc[aidx[3 * t]] != 0;                        // data[0].ca.disc, :340
@@ -213,7 +197,6 @@ __global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ cvb, c
     Vert app[3];
     uint32_t app_first = 0;
     bool appended = false;
-    const float half_w = sw / 2, half_h = sh / 2;
     if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear)            // :308
         appended = clip_tri(d, app, &app_first, textured, factor, half_w, half_h);
     setup_tri(d, textured, sw, sh, &tris[t]);
@@ -236,13 +219,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #define S3R_IT(p)
 #endif
 
-// ------------------------------------------------------------------ K3: row starts
+// ------------------------------------------------------------------ K3: row and segment starts
 // rowtab[((slot * H + y) * (segs + 1) + j) * 4 + c], component c of the exact walk of row y
 // (render.cpp:374-379):  j = 0: at x = xmin, i.e. weight.wy after y - ymin steps of dy;
 // j = 1 + s: at x = s * segw, the first pixel of fragment segment s, for every segment boundary
-// inside (xmin, xmax].  One lane per (slot, row, component): one O(binades) walk along the row.
+// inside (xmin, xmax].  k_rowstart: one lane per (slot, row, component); k_segstart: one lane per
+// (slot, row, component, segment boundary), each walking from the row start -- so the critical
+// path is one row walk plus one partial-row walk.
 __global__ void __launch_bounds__(192) k_rowstart(const TriSetup *__restrict__ tris, uint32_t H, uint32_t segs,
-                                                  uint32_t segw, float *__restrict__ rowtab) {
+                                                  float *__restrict__ rowtab) {
     const uint32_t slot = blockIdx.x;
     const uint32_t y = blockIdx.y * 64u + threadIdx.x;
     const uint32_t c = threadIdx.y;
@@ -251,30 +236,37 @@ __global__ void __launch_bounds__(192) k_rowstart(const TriSetup *__restrict__ t
     if (h0.x == kDead) return;
     const uint32_t ymax = reinterpret_cast<const uint4 *>(t)[1].x;
     if (y < h0.w || y > ymax || y >= H) return;
-    float *dst = rowtab + ((size_t)slot * H + y) * (segs + 1) * 4 + c;
-    const float d = t->dx[c];
 #ifdef S3R_STATS
-    uint32_t it_row = 0, it_seg = 0;
-    float v = exact_walk(t->ws[c], t->dy[c], y - h0.w, &it_row);
-#else
-    float v = exact_walk(t->ws[c], t->dy[c], y - h0.w);
-#endif
-    dst[0] = v;
-    uint32_t kpos = h0.y;
-    for (uint32_t sg = h0.y / segw + 1u; sg < segs && sg * segw <= h0.z; sg++) {
-#ifdef S3R_STATS
-        v = exact_walk(v, d, sg * segw - kpos, &it_seg);
-#else
-        v = exact_walk(v, d, sg * segw - kpos);
-#endif
-        kpos = sg * segw;
-        dst[(1 + sg) * 4] = v;
-    }
-#ifdef S3R_STATS
+    uint32_t it_row = 0;
+    rowtab[((size_t)slot * H + y) * (segs + 1) * 4 + c] = exact_walk(t->ws[c], t->dy[c], y - h0.w, &it_row);
     atomicAdd(&g_stats[12], (unsigned long long)it_row);
     atomicMax(&g_stats[13], (unsigned long long)it_row);
-    atomicAdd(&g_stats[14], (unsigned long long)it_seg);
-    atomicMax(&g_stats[15], (unsigned long long)it_seg);
+#else
+    rowtab[((size_t)slot * H + y) * (segs + 1) * 4 + c] = exact_walk(t->ws[c], t->dy[c], y - h0.w);
+#endif
+}
+
+__global__ void __launch_bounds__(256) k_segstart(const TriSetup *__restrict__ tris, uint32_t H, uint32_t segs,
+                                                  uint32_t segw, float *__restrict__ rowtab) {
+    const uint32_t slot = blockIdx.x;
+    const uint32_t y = blockIdx.y * 64u + threadIdx.x;
+    const uint32_t c = blockIdx.z % 3u;
+    const uint32_t sg = (blockIdx.z / 3u) * 4u + threadIdx.y + 1u;      // boundaries 1 .. segs-1
+    const TriSetup *t = tris + slot;
+    const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
+    if (h0.x == kDead) return;
+    const uint32_t ymax = reinterpret_cast<const uint4 *>(t)[1].x;
+    if (y < h0.w || y > ymax || y >= H || sg >= segs) return;
+    const uint32_t xb = sg * segw;
+    if (xb <= h0.y || xb > h0.z) return;
+    float *row = rowtab + ((size_t)slot * H + y) * (segs + 1) * 4 + c;
+#ifdef S3R_STATS
+    uint32_t it = 0;
+    row[(1 + sg) * 4] = exact_walk(row[0], t->dx[c], xb - h0.y, &it);
+    atomicAdd(&g_stats[14], (unsigned long long)it);
+    atomicMax(&g_stats[15], (unsigned long long)it);
+#else
+    row[(1 + sg) * 4] = exact_walk(row[0], t->dx[c], xb - h0.y);
 #endif
 }
 
@@ -295,8 +287,17 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint
 constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + component (63 lanes)
 constexpr uint32_t kWaves = 4;         // one wave per row: a workgroup is 4 consecutive local rows
 constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
-constexpr uint32_t kStateBatches = 4;  // batches whose walk state persists in LDS across chunks
-constexpr uint32_t kTables = 12;       // per wave: 64-entry exact-value tables for non-linear chunks
+#ifndef S3R_STATE_BATCHES
+#define S3R_STATE_BATCHES 4
+#endif
+#ifndef S3R_TABLES
+#define S3R_TABLES 12
+#endif
+#ifndef S3R_OCC
+#define S3R_OCC 6                      // target waves per SIMD (LDS allows 6 at the defaults)
+#endif
+constexpr uint32_t kStateBatches = S3R_STATE_BATCHES;  // batches whose walk state persists in LDS
+constexpr uint32_t kTables = S3R_TABLES;  // per wave: 64-entry exact-value tables, non-linear chunks
 
 struct Entry {                         // 48 B per listed triangle (LDS, shared by the 4 waves)
     uint32_t slot, xmin, xmax, ymin;
@@ -311,15 +312,19 @@ struct FragShared {
     uint32_t cnt, next;
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
-    float rc[kWaves][64], rd[kWaves][64];
-    uint32_t rt[kWaves][64];             // per (triangle, component) lane: table index, or kNoTable
-    uint32_t k0s[kWaves][kTPB + 3];
     float tab[kWaves][kTables][64];      // exact S(c, d, k), k = 0..63, filled by sequential adds
 };
 constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask, uint32_t lane) {
     return (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ float rdl(float v, uint32_t l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
 // LDS hand-off between lanes of ONE wave: LDS operations of a wave execute in order, so only the
@@ -437,7 +442,7 @@ __device__ __noinline__ uint32_t shade(const TriSetup *__restrict__ tp, float w0
 // that component's exact walk (render.cpp:374) to the chunk, publishing (value, step) in LDS; then
 // its lanes act as pixels: edge test, 1/z, strict '>' depth test in registers; the winner is shaded.
 template <uint32_t SEGCH>
-__global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
+__global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
@@ -460,8 +465,6 @@ __global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ t
     const uint32_t tl = lane / 3u, comp = lane - 3u * tl;                  // (triangle, component) role
     float *st_c = sh.st_c[wave];
     uint32_t *st_k = sh.st_k[wave];
-    float *rc = sh.rc[wave], *rd = sh.rd[wave];
-    uint32_t *k0s = sh.k0s[wave];
 #ifdef S3R_STATS
     uint32_t st_row = 0, st_chunk = 0, st_pix = 0, st_irr = 0, st_tests = 0, st_batches = 0;
     uint32_t *p_chunk = &st_chunk, *p_pix = &st_pix;
@@ -509,18 +512,21 @@ __global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ t
                 // ---- lanes as (triangle, component): advance the exact walk to this chunk
                 const uint32_t idx = b * kTPB + tl;
                 bool ov = false, lin = false, neg = false;
-                float c = 0.0f, d = 0.0f, del = 0.0f;
-                uint32_t k0 = 0, m = 0;
+                float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f;
+                uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
                 if (lane < 63 && idx < cnt) {
                     const Entry &e = sh.ent[idx];
                     ov = y >= e.ymin && y <= e.ymax && e.xmin <= cx1 && e.xmax >= cx0;
                     if (ov) {
                         d = e.dx[comp];
+                        rz = e.rvz[comp];
+                        xmax = e.xmax;
+                        slot = e.slot;
                         k0 = max(cx0, e.xmin);
                         m = min(cx1, e.xmax) - k0 + 1u;
                         if (stateful) {
-                            // state = exact value at pixel kp (the segment start / xmin, or the last
-                            // pixel of the previous chunk); contiguous chunks need 0 or 1 step
+                            // state = exact value at pixel kp (xmin or the segment start, or the last
+                            // pixel of the previous chunk): contiguous chunks need 0 or 1 step
                             const uint32_t kp = st_k[b * 64 + lane];
                             const float cp = st_c[b * 64 + lane];
                             c = k0 == kp ? cp : (k0 == kp + 1u ? cp + d : walk(cp, d, k0 - kp S3R_IT(p_chunk)));
@@ -531,7 +537,6 @@ __global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ t
                         }
                         lin = chunk_linear(c, d, m, &del);
                         if (lin) neg = c < 0.0f && c + (float)(m - 1u) * del < 0.0f;   // monotone walk
-                        if (comp == 0) k0s[tl] = k0;
                     }
                 }
                 const uint64_t ovm = __ballot(ov && comp == 0);
@@ -562,55 +567,49 @@ __global__ void __launch_bounds__(256) k_fragment(const TriSetup *__restrict__ t
                     }
                 }
                 negm = __ballot(neg);
-                if (ov) {
-                    rc[lane] = c;
-                    rd[lane] = del;
-                    sh.rt[wave][lane] = tix;
-                    if (stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = k0 + m - 1u; }
-                }
-                wave_sync();
+                if (ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = k0 + m - 1u; }
+                if (irrm) wave_sync();
 #ifdef S3R_STATS
                 st_batches++;
                 st_irr += (ov && !lin) ? 1u : 0u;
 #endif
-                // ---- lanes as pixels: triangles in slot order (bit 3t of `live`)
+                // ---- lanes as pixels: triangles in slot order (bit 3t of `live`); the (triangle,
+                // component) values are broadcast from their lanes with v_readlane
                 const uint64_t neg3 = negm | (negm >> 1) | (negm >> 2);
                 uint64_t live = ovm & ~neg3 & 0x9249249249249249ull;   // bits 0, 3, 6, ...
                 while (live) {
-                    const uint32_t t = (uint32_t)__builtin_ctzll(live) / 3u;
+                    const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
                     live &= live - 1;
-                    const Entry &e = sh.ent[b * kTPB + t];
-                    const uint32_t tk0 = k0s[t];
-                    if (x < tk0 || x > e.xmax) continue;
+                    const uint32_t tk0 = rdl(k0, l0), txmax = rdl(xmax, l0);
+                    if (x < tk0 || x > txmax) continue;
 #ifdef S3R_STATS
                     st_tests++;
 #endif
                     const uint32_t off = x - tk0;
                     const float fo = (float)off;
-                    float a[3];
+                    float a[3], r[3];
 #pragma unroll
-                    for (int cc = 0; cc < 3; cc++) {
-                        const uint32_t l = 3u * t + cc;
-                        const uint32_t ti = sh.rt[wave][l];
+                    for (uint32_t cc = 0; cc < 3; cc++) {
+                        const uint32_t l = l0 + cc;
+                        const float cv = rdl(c, l), dv = rdl(del, l);
+                        const uint32_t ti = rdl(tix, l);
+                        r[cc] = rdl(rz, l);
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
-                        a[cc] = rc[l] + fo * rd[l];
+                        a[cc] = cv + fo * dv;
 #else
-                        if (ti == kNoTable && !((irrm >> l) & 1ull))
-                            a[cc] = rc[l] + fo * rd[l];
-                        else if (ti != kNoTable)
-                            a[cc] = sh.tab[wave][ti][off];
-                        else
-                            a[cc] = walk(rc[l], e.dx[cc], off S3R_IT(p_pix));
+                        if (ti != kNoTable) a[cc] = sh.tab[wave][ti][off];
+                        else if (!((irrm >> l) & 1ull)) a[cc] = cv + fo * dv;
+                        else a[cc] = walk(cv, rdl(d, l), off S3R_IT(p_pix));
 #endif
                     }
-                    if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                                  // :362
-                        const float ooz = (e.rvz[0] * a[0] + e.rvz[1] * a[1]) + e.rvz[2] * a[2]; // :363
-                        if (ooz > depth) {                                                         // :364
-                            depth = ooz; win = (int)e.slot; bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
+                    if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
+                        const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
+                        if (ooz > depth) {                                              // :364
+                            depth = ooz; win = (int)rdl(slot, l0); bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
                         }
                     }
                 }
-                wave_sync();
+                if (irrm) wave_sync();
             }
             if (!overflow || cursor >= nslots) break;
         }
@@ -665,24 +664,17 @@ void stats_read(unsigned long long out[16], bool reset) {
 }
 
 // ------------------------------------------------------------------ launchers
-constexpr uint32_t kSegChunks = 16;   // 1024-pixel segments
+#ifndef S3R_SEG_CHUNKS
+#define S3R_SEG_CHUNKS 6
+#endif
+constexpr uint32_t kSegChunks = S3R_SEG_CHUNKS;   // 64-pixel chunks per fragment segment
 
-void launch_vertex(const float4 *vtx, uint32_t nv, const float4 *nrm, uint32_t na, const Mat34 &m,
-                   float factor, float sw, float sh, float4 *cv, float4 *rv, float4 *ncam, hipStream_t st) {
-    const uint32_t n = nv > na ? nv : na;
-    if (n == 0) return;
-    uint32_t blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_vertex, dim3(blocks), dim3(256), 0, st, vtx, nv, nrm, na, m, factor, sw / 2,
-                       sh / 2, cv, rv, ncam);
-}
-
-void launch_setup(const float4 *cv, const float4 *rv, const float4 *ncam, const float4 *pay,
-                  const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
-                  float factor, float sw, float sh, TriSetup *tris, hipStream_t st) {
+void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
+                  const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
+                  float sw, float sh, TriSetup *tris, hipStream_t st) {
     if (ntri == 0) return;
-    hipLaunchKernelGGL(k_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, cv, rv, ncam, pay, disc, vidx,
-                       aidx, ntri, factor, sw, sh, tris);
+    hipLaunchKernelGGL(k_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, nrm, pay, disc, vidx, aidx, ntri,
+                       m, factor, sw, sh, tris);
 }
 
 uint32_t fragment_segment_pixels() { return 64u * kSegChunks; }
@@ -691,8 +683,11 @@ uint32_t fragment_segments(uint32_t W) { return (W + 64u * kSegChunks - 1) / (64
 
 void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st) {
     if (nslots == 0 || H == 0) return;
-    hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, fragment_segments(W),
-                       64u * kSegChunks, rowtab);
+    const uint32_t segs = fragment_segments(W);
+    hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, segs, rowtab);
+    if (segs > 1)
+        hipLaunchKernelGGL(k_segstart, dim3(nslots, (H + 63) / 64, 3 * ((segs - 1 + 3) / 4)), dim3(64, 4), 0, st,
+                           tris, H, segs, 64u * kSegChunks, rowtab);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

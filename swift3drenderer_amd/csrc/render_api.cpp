@@ -55,14 +55,16 @@ struct Lib {
     float4 *vtx = nullptr, *nrm = nullptr, *pay = nullptr;
     uint8_t *disc = nullptr;
     uint32_t *vidx = nullptr, *aidx = nullptr, *tex = nullptr;
-    // per-frame scratch
-    float4 *cv = nullptr, *rv = nullptr, *ncam = nullptr;
-    TriSetup *tris = nullptr;
+    // per-frame geometry, double-buffered: frame k's geometry (k_setup, k_rowstart on stream `geo`)
+    // overlaps frame k-1's fragment kernel on the caller's stream
+    TriSetup *tris[2] = {nullptr, nullptr};
+    float *rowtab[2] = {nullptr, nullptr};     // 2T x H x (segments + 1) x float4 exact row starts
+    size_t rowtab_cap = 0;
+    hipEvent_t geo_done[2] = {nullptr, nullptr}, frag_done[2] = {nullptr, nullptr};
+    uint32_t parity = 0;
     uint32_t *frame = nullptr;
     size_t frame_cap = 0;
-    float *rowtab = nullptr;       // 2T x H x float4 exact row starts
-    size_t rowtab_cap = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr, geo = nullptr;
 
     // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
     struct Reg { void *p; size_t n; bool ok; };
@@ -211,8 +213,12 @@ void initialize() {
     g.disc = dalloc<uint8_t>(na);
     g.vidx = dalloc<uint32_t>(3 * ntri); g.aidx = dalloc<uint32_t>(3 * ntri);
     g.tex = dalloc<uint32_t>(nt);
-    g.cv = dalloc<float4>(nv); g.rv = dalloc<float4>(nv); g.ncam = dalloc<float4>(na);
-    g.tris = dalloc<TriSetup>(2 * ntri);
+    for (int p = 0; p < 2; p++) {
+        g.tris[p] = dalloc<TriSetup>(2 * ntri);
+        HIPCHECK(hipEventCreateWithFlags(&g.geo_done[p], hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&g.frag_done[p], hipEventDisableTiming));
+    }
+    if (!g.geo) HIPCHECK(hipStreamCreateWithFlags(&g.geo, hipStreamNonBlocking));
     HIPCHECK(hipMemcpy(g.vtx, vtx.data(), nv * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(g.nrm, nrm.data(), na * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(g.pay, pay.data(), na * 16, hipMemcpyHostToDevice));
@@ -232,11 +238,18 @@ void release_all() {
     if (g.initialized) {
         (void)hipSetDevice(g.device);
         if (g.stream) (void)hipStreamSynchronize(g.stream);
+        if (g.geo) (void)hipStreamSynchronize(g.geo);
+        (void)hipDeviceSynchronize();
         unregister_all();
-        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.cv, g.rv, g.ncam, g.tris, g.frame,
-                        g.rowtab};
+        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.tris[0], g.tris[1], g.frame,
+                        g.rowtab[0], g.rowtab[1]};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
+        for (int p = 0; p < 2; p++) {
+            if (g.geo_done[p]) (void)hipEventDestroy(g.geo_done[p]);
+            if (g.frag_done[p]) (void)hipEventDestroy(g.frag_done[p]);
+        }
+        if (g.geo) (void)hipStreamDestroy(g.geo);
         for (auto &t : g.tslots) {
             (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
         }
@@ -281,21 +294,30 @@ TimingSlot *timing_slot() {
 void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st) {
     TimingSlot *ts = timing_slot();
-    if (ts) HIPCHECK(hipEventRecord(ts->frame0, st));
     const float sw = (float)W, sh = (float)H;
-    launch_vertex(g.vtx, g.nv, g.nrm, g.na, g.m, g.factor, sw, sh, g.cv, g.rv, g.ncam, st);
-    launch_setup(g.cv, g.rv, g.ncam, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.factor, sw, sh, g.tris, st);
     const size_t need = (size_t)2 * g.ntri * H * (fragment_segments(W) + 1) * 4;
     if (g.rowtab_cap < need) {
-        HIPCHECK(hipStreamSynchronize(st));
-        if (g.rowtab) HIPCHECK(hipFree(g.rowtab));
-        g.rowtab = dalloc<float>(need);
+        HIPCHECK(hipDeviceSynchronize());
+        for (int p = 0; p < 2; p++) {
+            if (g.rowtab[p]) HIPCHECK(hipFree(g.rowtab[p]));
+            g.rowtab[p] = dalloc<float>(need);
+        }
         g.rowtab_cap = need;
     }
-    launch_rowstart(g.tris, 2 * g.ntri, W, H, g.rowtab, st);
+    // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
+    const uint32_t p = g.parity;
+    g.parity ^= 1u;
+    HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
+    if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
+    launch_setup(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh, g.tris[p], g.geo);
+    launch_rowstart(g.tris[p], 2 * g.ntri, W, H, g.rowtab[p], g.geo);
+    HIPCHECK(hipEventRecord(g.geo_done[p], g.geo));
+    // fragment on the caller's stream
+    HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_fragment(g.tris, 2 * g.ntri, g.rowtab, g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
+    launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
+    HIPCHECK(hipEventRecord(g.frag_done[p], st));
     HIPCHECK(hipGetLastError());
 }
 

@@ -66,14 +66,14 @@ S3R_HD float regular_steps(float s, float d, float delta, uint32_t e) {
     const float A = fabsf(delta) * inv_u;
     const float D = fabsf(d) * inv_u;
     const bool away = (s > 0.0f) == (delta > 0.0f);
-    const float N = away ? (pow2_biased(e + 1u) - as) * inv_u - floorf(D) - 1.0f
-                         : (as - pow2_biased(e)) * inv_u - ceilf(D);
-    if (N < 0.0f) return 0.0f;
+    const float n_away = (pow2_biased(e + 1u) - as) * inv_u - floorf(D) - 1.0f;
+    const float n_towards = (as - pow2_biased(e)) * inv_u - ceilf(D);
+    const float N = away ? n_away : n_towards;
     float q = floorf(quot_approx(N, A));                  // ~1 ulp; corrected exactly below
-    if (q * A > N) q -= 1.0f;
-    if (q * A > N) q -= 1.0f;
-    if ((q + 1.0f) * A <= N) q += 1.0f;
-    return q + 1.0f;
+    q = q * A > N ? q - 1.0f : q;
+    q = q * A > N ? q - 1.0f : q;
+    q = (q + 1.0f) * A <= N ? q + 1.0f : q;
+    return N >= 0.0f ? q + 1.0f : 0.0f;                  // (NaN for out-of-range e: never selected)
 }
 
 // exact_walk(s, d, n) == the float32 value after n sequential steps s = fl(s + d)
@@ -89,25 +89,25 @@ S3R_HD float exact_walk(float s, float d, uint32_t n, uint32_t *iters = nullptr)
     if (n == 0) return s;
     const float ad = fabsf(d);
     if (ad == 0.0f || !is_finite(s) || !is_finite(d)) return s + d;   // one add is a fixed point
-    while (n) {
+    const float ad4 = 4.0f * ad, ad8 = 8.0f * ad;
+    // Branch-free body: every iteration computes the single step and the maximal jump and selects,
+    // so the lanes of a wave only diverge at the loop exit.
+    while (n != 0u) {
         if (iters) ++*iters;
         const float as = fabsf(s);
         const bool towards_zero = (s < 0.0f) != (d < 0.0f);
-        if (!(as >= 4.0f * ad) || (towards_zero && as < 8.0f * ad)) { s = s + d; --n; continue; }
         const float s1 = s + d;
-        if (n == 1) return s1;
         const float s2 = s1 + d;
         const uint32_t e = fexp(s);
-        if (e < 32u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - s) != (s2 - s1)) {
-            s = s1; --n; continue;
-        }
-        const float delta = s1 - s;           // exact (same binade)
-        if (delta == 0.0f) return s;          // fl(s + d) == s: stagnated for good
-        float j = regular_steps(s, d, delta, e);
-        if (j < 2.0f) { s = s1; --n; continue; }
-        if (j > (float)n) j = (float)n;
-        s = s + j * delta;                    // exact: lands on the grid, at most on the edge
-        n -= (uint32_t)j;
+        const float delta = s1 - s;           // exact whenever `steady`
+        // non-short-circuit '&' keeps hipcc from turning the test into nested branches
+        const bool steady = (as >= ad4) & !(towards_zero & (as < ad8)) & (n >= 2u) & (e >= 32u) & (e < 254u) &
+                            (fexp(s1) == e) & (fexp(s2) == e) & (delta == s2 - s1);
+        if (steady & (delta == 0.0f)) break;  // fl(s + d) == s: stagnated for good
+        float j = fminf(regular_steps(s, d, delta, e), (float)n);
+        const bool jump = steady & (j >= 2.0f);
+        s = jump ? s + j * delta : s1;        // exact: lands on the grid, at most on the edge
+        n -= jump ? (uint32_t)j : 1u;
     }
     return s;
 }
@@ -122,14 +122,14 @@ S3R_HD bool chunk_linear(float c, float d, uint32_t m, float *delta) {
     if (ad == 0.0f) return c != 0.0f;                     // c + 0 == c unless c is -0
     const float ac = fabsf(c);
     const bool towards_zero = (c < 0.0f) != (d < 0.0f);
-    if (!(ac >= 4.0f * ad) || (towards_zero && ac < 8.0f * ad)) return false;
     const float s1 = c + d, s2 = s1 + d;
     const uint32_t e = fexp(c);
-    if (e < 32u || e >= 254u || fexp(s1) != e || fexp(s2) != e || (s1 - c) != (s2 - s1)) return false;
     const float del = s1 - c;
-    *delta = del;
-    if (del == 0.0f) return true;
-    return regular_steps(c, d, del, e) >= (float)(m - 1u);   // m-1 regular steps reach the chunk end
+    const bool steady = (ac >= 4.0f * ad) & !(towards_zero & (ac < 8.0f * ad)) & (e >= 32u) & (e < 254u) &
+                        (fexp(s1) == e) & (fexp(s2) == e) & (del == s2 - s1);
+    *delta = steady ? del : 0.0f;
+    // m-1 regular steps reach the chunk end (or the walk has stagnated: del == 0)
+    return steady & ((del == 0.0f) | (regular_steps(c, d, del, e) >= (float)(m - 1u)));
 }
 
 // ---- float3 helpers in the reference's evaluation order ----

@@ -4,12 +4,9 @@
 
 namespace s3r {
 
-void launch_vertex(const float4 *vtx, uint32_t nv, const float4 *nrm, uint32_t na, const Mat34 &m,
-                   float factor, float sw, float sh, float4 *cv, float4 *rv, float4 *ncam, hipStream_t st);
-
-void launch_setup(const float4 *cv, const float4 *rv, const float4 *ncam, const float4 *pay,
-                  const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
-                  float factor, float sw, float sh, TriSetup *tris, hipStream_t st);
+void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
+                  const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
+                  float sw, float sh, TriSetup *tris, hipStream_t st);
 
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
