@@ -42,6 +42,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=10.0, help='CPU-baseline sample budget')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-e2e', action='store_true')
+    p.add_argument('--backend', default='nccl', help="torch.distributed backend: nccl (RCCL) or gloo "
+                   "(rehearsal only: gathers through host memory)")
     return p.parse_args()
 
 
@@ -101,10 +103,14 @@ def main():
     dev = torch.device('cuda', local)
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl', device_id=dev)
+        if a.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
 
     from swift3drenderer_amd import poses, scene
-    from swift3drenderer_amd.renderer import Renderer, band_row_ids
+    from swift3drenderer_amd.multi import BandGather
+    from swift3drenderer_amd.renderer import Renderer
 
     tmp = tempfile.mkdtemp(prefix=f's3r_bench_{rank}_')
     data_path = os.path.join(tmp, f'{a.scene}.bin')
@@ -121,21 +127,20 @@ def main():
     rows = r.lib.s3r_band_rows_local(H, B, N, rank) if N > 1 else H
     local_buf = torch.empty((max(rows, 1), W), dtype=torch.int32, device=dev)
     if N > 1:
-        max_rows = max(r.lib.s3r_band_rows_local(H, B, N, p) for p in range(N))
-        send = torch.zeros((max_rows, W), dtype=torch.int32, device=dev)
-        recv = [torch.empty((max_rows, W), dtype=torch.int32, device=dev) for _ in range(N)] if rank == 0 else None
-        frame = torch.empty((H, W), dtype=torch.int32, device=dev) if rank == 0 else None
-        ids = [torch.as_tensor(band_row_ids(H, B, N, p), device=dev) for p in range(N)]
+        # gloo rehearsal (one box, ranks sharing a GPU): the same gather through host memory
+        gdev = dev if a.backend == 'nccl' else torch.device('cpu')
+        bg = BandGather(W, H, B, N, rank, gdev)
 
     def step(inp):
         if N == 1:
             r.render_bands(inp, W, H, H, 1, 0, local_buf.data_ptr(), sptr)
             return
-        r.render_bands(inp, W, H, B, N, rank, send.data_ptr(), sptr)
-        dist.gather(send, recv, dst=0)
-        if rank == 0:
-            for p in range(N):
-                frame.index_copy_(0, ids[p], recv[p][: ids[p].numel()])
+        if a.backend == 'nccl':
+            r.render_bands(inp, W, H, B, N, rank, bg.send.data_ptr(), sptr)   # straight into the send buffer
+        else:
+            r.render_bands(inp, W, H, B, N, rank, local_buf.data_ptr(), sptr)
+            bg.send[:rows].copy_(local_buf[:rows].cpu())
+        bg.gather()
 
     for t in script:                     # pose script (first call initialises), untimed
         step(t)

@@ -1,0 +1,58 @@
+"""Multi-GPU frame assembly: interleaved row bands + one gather (RCCL over xGMI on MI355X).
+
+SURVEY.md §8e: every rank holds the whole (small) scene, runs the geometry stage redundantly and
+rasterizes only its rows -- frame row y belongs to rank (y // band) % world -- into a compact local
+buffer (the library's ``s3r_render_bands``).  One ``gather`` brings the bands to rank 0, which
+scatters them back into frame order.  With ``torch.distributed`` on the ``nccl`` backend the gather
+is RCCL; the ``gloo`` backend runs the same code on CPU tensors (tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def band_row_ids(height: int, band: int, nparts: int, part: int) -> np.ndarray:
+    """Frame rows owned by `part`, in local storage order (increasing y)."""
+    y = np.arange(height)
+    return y[(y // band) % nparts == part]
+
+
+def band_rows(height: int, band: int, nparts: int, part: int) -> int:
+    return int(((np.arange(height) // band) % nparts == part).sum())
+
+
+class BandGather:
+    """Per-run buffers for gathering a W x H frame split into `world` interleaved parts."""
+
+    def __init__(self, width: int, height: int, band: int, world: int, rank: int, device):
+        self.W, self.H, self.B, self.N, self.rank = width, height, band, world, rank
+        self.rows = band_rows(height, band, world, rank)
+        self.max_rows = max(band_rows(height, band, world, p) for p in range(world))
+        self.send = torch.zeros((self.max_rows, width), dtype=torch.int32, device=device)
+        self.recv = None
+        self.frame = None
+        if rank == 0:
+            self.recv = [torch.empty((self.max_rows, width), dtype=torch.int32, device=device) for _ in range(world)]
+            self.frame = torch.empty((height, width), dtype=torch.int32, device=device)
+            self.ids = [torch.as_tensor(band_row_ids(height, band, world, p), device=device) for p in range(world)]
+
+    def gather(self, group=None):
+        """Collective: every rank's `send` (rows [0, rows) valid) -> rank 0's `frame`."""
+        dist.gather(self.send, self.recv, dst=0, group=group)
+        if self.rank == 0:
+            for p in range(self.N):
+                self.frame.index_copy_(0, self.ids[p], self.recv[p][: self.ids[p].numel()])
+        return self.frame
+
+
+def assemble(parts, height: int, band: int) -> np.ndarray:
+    """Host-side reassembly of per-part compact buffers (tests and single-process use)."""
+    n = len(parts)
+    w = parts[0].shape[1]
+    out = np.empty((height, w), dtype=parts[0].dtype)
+    for p, buf in enumerate(parts):
+        ids = band_row_ids(height, band, n, p)
+        out[ids] = buf[: len(ids)]
+    return out
