@@ -99,6 +99,8 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit('--gpus N>1 needs torch.distributed.run with N processes')
+    # one process per GPU; on a box with fewer GPUs than ranks (a gloo rehearsal) ranks share them
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:

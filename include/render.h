@@ -57,8 +57,10 @@ void s3r_shutdown(void);
 /* One frame for one part of an interleaved row-band split (multi-GPU).  Same camera / init /
  * resize semantics as updateAndRender.  Frame row y belongs to part ((y / band_rows) % n_parts);
  * this part's rows are written compactly, in increasing y, to the DEVICE buffer dev_out
- * (rows_local x width u32), asynchronously on `stream` (a hipStream_t; NULL = the library's own
- * stream).  n_parts = 1 renders the whole frame.  Returns rows_local, or -1 on bad arguments. */
+ * (rows_local x width u32), asynchronously on `stream` (a hipStream_t; NULL = the default (null)
+ * stream).  The geometry stage runs on an internal stream and is ordered with `stream` by events,
+ * so frame k+1's geometry overlaps frame k's fragment kernel.  n_parts = 1 renders the whole
+ * frame.  Returns rows_local, or -1 on bad arguments. */
 int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height, uint32_t band_rows,
                          uint32_t n_parts, uint32_t part, uint32_t *dev_out, void *stream);
 

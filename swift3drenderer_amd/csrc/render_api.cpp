@@ -383,7 +383,8 @@ __attribute__((visibility("default"))) int64_t s3r_render_bands(const Input *inp
     if (band_rows == 0 || n_parts == 0 || part >= n_parts || (!dev_out && width && height)) return -1;
     frame_begin(input, width, height);
     const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
-    hipStream_t st = stream ? (hipStream_t)stream : g.stream;
+    // NULL is the legacy default (null) stream -- e.g. torch's default stream -- never our own.
+    hipStream_t st = (hipStream_t)stream;
     if (rows && width) render_core(width, height, band_rows, n_parts, part, rows, dev_out, st);
     return rows;
 }

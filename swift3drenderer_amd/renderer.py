@@ -79,7 +79,8 @@ class Renderer:
 
     def render_bands(self, inp, width: int, height: int, band: int, nparts: int, part: int, dev_ptr: int,
                      stream: int = 0) -> int:
-        """Render one part of an interleaved row-band split into device memory at dev_ptr."""
+        """Render one part of an interleaved row-band split into device memory at dev_ptr, on the
+        HIP stream `stream` (0 = the default stream, i.e. torch's default stream)."""
         i = Input.of(inp)
         r = self.lib.s3r_render_bands(ctypes.byref(i), width, height, band, nparts, part,
                                       ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None))
