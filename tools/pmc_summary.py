@@ -1,31 +1,60 @@
 #!/usr/bin/env python3
-"""Average each PMC counter per dispatch of each kernel over the pass directories of tools/pmc.sh."""
+"""Per-kernel PMC averages over the last N dispatches (the bench's timed frames) of every pass
+directory under <dir>, and the HBM traffic of k_fragment per launch.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE (KiB, from the TCC EA request
+counters) each in their own pass; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
+reads, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (the read side is an upper bound for
+narrower accesses); WRITE_SIZE is exact for streaming stores.
+"""
+import argparse
 import csv
 import glob
 import json
 import os
-import sys
 from collections import defaultdict
 
 
-def main(d):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('dir')
+    ap.add_argument('--last', type=int, default=0)
+    ap.add_argument('--workload', default=None)
+    a = ap.parse_args()
     acc = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(d, 'p*', '**', '*counter_collection.csv'), recursive=True):
+    for f in sorted(glob.glob(os.path.join(a.dir, 'pmc*', '**', '*counter_collection.csv'), recursive=True)):
+        rows = defaultdict(lambda: defaultdict(float))
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                name = row.get('Kernel_Name', '')
-                short = name.split('(')[0].replace('void ', '')
-                acc[short][row['Counter_Name']].append(float(row['Counter_Value']))
+                short = row.get('Kernel_Name', '').split('(')[0].replace('void ', '')
+                rows[short][(int(row['Dispatch_Id']), row['Counter_Name'])] += float(row['Counter_Value'])
+        for k, d in rows.items():
+            ids = sorted({i for i, _ in d})
+            if a.last:
+                ids = ids[-a.last:]
+            for (i, c), val in d.items():
+                if i in ids:
+                    acc[k][c].append(val)
     out = {}
     for k, cs in acc.items():
         out[k] = {c: sum(v) / len(v) for c, v in cs.items()}
         out[k]['_dispatches'] = max(len(v) for v in cs.values())
-    json.dump(out, open(os.path.join(d, 'summary.json'), 'w'), indent=1)
+    with open(os.path.join(a.dir, 'pmc_summary.json'), 'w') as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
     for k, cs in out.items():
         print(k)
         for c in sorted(cs):
-            print(f'   {c:28s} {cs[c]:.4g}')
+            print(f'   {c:28s} {cs[c]:.6g}')
+    frag = next((v for k, v in out.items() if 'k_fragment' in k), None)
+    if frag and a.workload and 'FETCH_SIZE' in frag and 'WRITE_SIZE' in frag:
+        t = {a.workload: {'kernel': 'k_fragment', 'fetch_size_kib': frag['FETCH_SIZE'],
+                          'write_size_kib': frag['WRITE_SIZE'],
+                          'hbm_bytes_per_launch': int((2 * frag['FETCH_SIZE'] + frag['WRITE_SIZE']) * 1024),
+                          'formula': '(2*FETCH_SIZE + WRITE_SIZE) * 1024, MI355X_MICROARCH.md HBM section'}}
+        with open(os.path.join(a.dir, 'pmc_traffic.json'), 'w') as fh:
+            json.dump(t, fh, indent=1)
+        print(json.dumps(t))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    main()
