@@ -294,12 +294,12 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #define S3R_TABLES 12
 #endif
 #ifndef S3R_OCC
-#define S3R_OCC 6                      // target waves per SIMD (LDS allows 6 at the defaults)
+#define S3R_OCC 5                      // target waves per SIMD (5: no spills at <= 96 VGPRs)
 #endif
 constexpr uint32_t kStateBatches = S3R_STATE_BATCHES;  // batches whose walk state persists in LDS
 constexpr uint32_t kTables = S3R_TABLES;  // per wave: 64-entry exact-value tables, non-linear chunks
 
-struct Entry {                         // 48 B per listed triangle (LDS, shared by the 4 waves)
+struct alignas(16) Entry {              // 48 B per listed triangle (LDS, shared by the 4 waves)
     uint32_t slot, xmin, xmax, ymin;
     uint32_t ymax;
     float dx[3];
@@ -400,6 +400,57 @@ __device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, u
     __syncthreads();
 }
 
+// ------------------------------------------------------------------ K4a: binning
+// One wave per bin = (block of kWaves local rows) x (fragment segment): the live triangles whose
+// bbox meets it, in slot order (the reference's processing order), written as compact Entry records
+// so the fragment workgroup loads its list with one coalesced read.  counts[bin] = kListMax + 1
+// marks an overflowing bin: the fragment kernel then scans the slots itself, in rounds.
+__global__ void __launch_bounds__(256) k_bin(const TriSetup *__restrict__ tris, uint32_t nslots, uint32_t W,
+                                             uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+                                             uint32_t rows_local, uint32_t segs, uint32_t segw,
+                                             Entry *__restrict__ bins, uint32_t *__restrict__ counts) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t bin = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t nblk = (rows_local + kWaves - 1) / kWaves;
+    if (bin >= nblk * segs) return;
+    const uint32_t blk = bin / segs, seg = bin - blk * segs;
+    uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
+    for (uint32_t k = 0; k < kWaves && blk * kWaves + k < rows_local; k++) {
+        const uint32_t lr = blk * kWaves + k;
+        const uint32_t yy = ((lr / band) * nparts + part) * band + lr % band;
+        y0 = min(y0, yy); y1 = max(y1, yy);
+    }
+    const uint32_t x0 = seg * segw, x1 = min(W, x0 + segw) - 1u;
+    Entry *out = bins + (size_t)bin * kListMax;
+    uint32_t cnt = 0;
+    bool over = false;
+    for (uint32_t cursor = 0; cursor < nslots && !over; cursor += 64u) {
+        const uint32_t s = cursor + lane;
+        bool act = false;
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
+        if (s < nslots) {
+            h0 = reinterpret_cast<const uint4 *>(tris + s)[0];                   // kind xmin xmax ymin
+            h1 = reinterpret_cast<const uint4 *>(tris + s)[1];                   // ymax ...
+            act = h0.x != kDead && h0.w <= y1 && h1.x >= y0 && h0.y <= x1 && h0.z >= x0 && y0 < H;
+        }
+        const uint64_t mask = __ballot(act);
+        const uint32_t pc = (uint32_t)__builtin_popcountll(mask);
+        if (cnt + pc > kListMax) { over = true; break; }
+        if (act) {
+            const float4 dx = reinterpret_cast<const float4 *>(tris + s)[3];
+            const float4 rz = reinterpret_cast<const float4 *>(tris + s)[5];
+            Entry e;
+            e.slot = s; e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
+            e.dx[0] = dx.x; e.dx[1] = dx.y; e.dx[2] = dx.z;
+            e.rvz[0] = rz.x; e.rvz[1] = rz.y; e.rvz[2] = rz.z;
+            e.pad = 0;
+            out[cnt + lane_prefix(mask, lane)] = e;
+        }
+        cnt += pc;
+    }
+    if (lane == 0) counts[bin] = over ? kListMax + 1u : cnt;
+}
+
 // Deferred shading of the winning triangle (render.cpp:366-371).
 __device__ __noinline__ uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
                                        const uint32_t *__restrict__ tex, uint32_t ntex) {
@@ -436,6 +487,103 @@ __device__ __noinline__ uint32_t shade(const TriSetup *__restrict__ tp, float w0
     return rgb_pack(s * col.x, s * col.y, s * col.z);
 }
 
+// Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle.
+struct BatchLanes {
+    bool ov = false, lin = false, neg = false;
+    float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f;
+    uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
+};
+struct BatchMasks {
+    uint64_t ovm, negm, irrm;
+    uint32_t tix;
+};
+
+// Pruning and exact tables for one batch: a triangle with a component negative over the whole chunk
+// covers none of it; a non-linear component gets a 64-entry table filled by the reference's own
+// sequential loop (render.cpp:374).  `last` = the component's exact value at the chunk's last pixel
+// (or at its first, for a pruned non-linear component), the walk state for the next chunk.
+__device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32_t lane, float (*tab)[64],
+                                              BatchMasks &bm, float &last
+#ifdef S3R_STATS
+                                              , uint32_t *p_chunk
+#endif
+) {
+    bm.ovm = __ballot(v.ov && (lane - 3u * tl) == 0u);
+    bm.tix = kNoTable;
+    last = v.c + (float)(v.m - 1u) * v.del;
+    if (bm.ovm == 0) { bm.negm = bm.irrm = 0; return; }
+    bm.negm = __ballot(v.neg);
+    bm.irrm = __ballot(v.ov && !v.lin && !((bm.negm >> (3u * tl)) & 7ull));
+    if (v.ov && !v.lin) {
+        if ((bm.negm >> (3u * tl)) & 7ull) {
+            last = v.c;                       // pruned: keep the state at the chunk start
+            v.m = 1u;
+        } else {
+            const uint32_t r = lane_prefix(bm.irrm, lane);
+            if (r < kTables) {
+                float w = v.c;
+                float *tb = tab[r];
+                tb[0] = w;
+                for (uint32_t k = 1; k < v.m; k++) { w = w + v.d; tb[k] = w; }
+                last = w;
+                bm.tix = r;
+            } else {
+                last = walk(v.c, v.d, v.m - 1u S3R_IT(p_chunk));
+            }
+            v.neg = v.c < 0.0f && last < 0.0f;
+        }
+    }
+    bm.negm = __ballot(v.neg);
+    if (bm.irrm) wave_sync();
+}
+
+// Lanes as pixels: triangles in slot order (bit 3t of `live`); (triangle, component) values are
+// broadcast from their lanes with v_readlane.  Edge test, 1/z, strict '>' depth test in registers.
+__device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMasks &bm, uint32_t x, float (*tab)[64],
+                                            float &depth, int &win, float &bw0, float &bw1, float &bw2
+#ifdef S3R_STATS
+                                            , uint32_t *p_pix, uint32_t *p_tests
+#endif
+) {
+    const uint64_t neg3 = bm.negm | (bm.negm >> 1) | (bm.negm >> 2);
+    uint64_t live = bm.ovm & ~neg3 & 0x9249249249249249ull;   // bits 0, 3, 6, ...
+    while (live) {
+        const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
+        live &= live - 1;
+        const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0);
+        if (x < tk0 || x > txmax) continue;
+#ifdef S3R_STATS
+        (*p_tests)++;
+#endif
+        const uint32_t off = x - tk0;
+        const float fo = (float)off;
+        float a[3], r[3];
+#pragma unroll
+        for (uint32_t cc = 0; cc < 3; cc++) {
+            const uint32_t l = l0 + cc;
+            const float cv = rdl(v.c, l), dv = rdl(v.del, l);
+            r[cc] = rdl(v.rz, l);
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
+            a[cc] = cv + fo * dv;
+#else
+            if (!((bm.irrm >> l) & 1ull)) {
+                a[cc] = cv + fo * dv;                          // linear chunk (or pruned: unused)
+            } else {
+                const uint32_t ti = rdl(bm.tix, l);
+                a[cc] = ti != kNoTable ? tab[ti][off] : walk(cv, rdl(v.d, l), off S3R_IT(p_pix));
+            }
+#endif
+        }
+        if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
+            const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
+            if (ooz > depth) {                                              // :364
+                depth = ooz; win = (int)rdl(v.slot, l0); bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
+            }
+        }
+    }
+    if (bm.irrm) wave_sync();
+}
+
 // A workgroup = 4 waves = 4 consecutive local rows x one segment of SEGCH 64-pixel chunks.  The
 // triangles meeting that block are listed once in LDS (slot order).  For each chunk, each wave takes
 // them kTPB at a time: its lanes first act as (triangle, barycentric component) pairs and advance
@@ -446,7 +594,8 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
-                                                  uint32_t rows_local) {
+                                                  uint32_t rows_local, const Entry *__restrict__ bins,
+                                                  const uint32_t *__restrict__ counts) {
     __shared__ FragShared sh;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t blk = blockIdx.x / segs, seg = blockIdx.x - blk * segs;
@@ -470,10 +619,34 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
     uint32_t *p_chunk = &st_chunk, *p_pix = &st_pix;
 #endif
 
-    build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
+    // this workgroup's triangle list, binned by k_bin (one coalesced read), or, for an overflowing
+    // bin, the first round of an in-kernel slot scan
+    const uint32_t bcount = counts[blockIdx.x];
+    bool overflow;
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 32)
+    if (bcount <= kListMax + 100u) {      // ablation: no list load (garbage list, count forced to 0)
+        if (threadIdx.x == 0) sh.cnt = 0u * bcount;
+        __syncthreads();
+        overflow = false;
+    } else
+#endif
+    if (bcount <= kListMax) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(bins + (size_t)blockIdx.x * kListMax);
+        uint4 *dst = reinterpret_cast<uint4 *>(sh.ent);
+        for (uint32_t i = threadIdx.x; i < bcount * 3u; i += 64u * kWaves) dst[i] = src[i];
+        if (threadIdx.x == 0) sh.cnt = bcount;
+        __syncthreads();
+        overflow = false;
+    } else {
+        build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
+        overflow = sh.next < nslots;           // > kListMax triangles: stateless rounds per chunk
+    }
     const uint32_t n0 = sh.cnt;
-    const bool overflow = sh.next < nslots;   // > kListMax triangles: stateless rounds per chunk
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 16)
+    if (false) {
+#else
     if (!overflow && row_ok) {
+#endif
         // walk state of the first batches: the exact row start (rowtab) at x = xmin
         for (uint32_t b = 0; b < kStateBatches && b * kTPB < n0; b++) {
             const uint32_t idx = b * kTPB + tl;
@@ -491,6 +664,24 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
         wave_sync();
     }
 
+    // ---- batch 0 (the first kTPB listed triangles: nearly every row has no more) keeps its
+    // constants, walk state and current linear run in registers
+    const bool reg0 = !overflow && row_ok && n0 > 0;
+    bool r0_in = false;
+    float r0_d = 0.0f, r0_rz = 0.0f, r0_sc = 0.0f, r0_base = 0.0f, r0_del = 0.0f;
+    uint32_t r0_xmin = 1u, r0_xmax = 0u, r0_slot = 0u, r0_sk = 0u, r0_k = 1u, r0_end = 0u;
+    if (reg0 && lane < 63 && tl < n0) {
+        const Entry &e = sh.ent[tl];
+        r0_in = y >= e.ymin && y <= e.ymax;
+        r0_d = e.dx[comp];
+        r0_rz = e.rvz[comp];
+        r0_xmin = e.xmin;
+        r0_xmax = e.xmax;
+        r0_slot = e.slot;
+        r0_sc = st_c[lane];
+        r0_sk = st_k[lane];
+    }
+
     uint32_t *row = out + (size_t)lr * W;
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + 64u * q;
@@ -500,6 +691,55 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
         float depth = 0.0f, bw0 = 0.0f, bw1 = 0.0f, bw2 = 0.0f;
         int win = -1;
 
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 8)
+        if (false) {
+#else
+        if (reg0) {
+#endif
+            BatchLanes v;
+            if (r0_in && r0_xmin <= cx1 && r0_xmax >= cx0) {
+                v.ov = true;
+                v.d = r0_d; v.rz = r0_rz; v.xmax = r0_xmax; v.slot = r0_slot;
+                v.k0 = max(cx0, r0_xmin);
+                const uint32_t kend = min(cx1, r0_xmax);
+                v.m = kend - v.k0 + 1u;
+                if (v.k0 >= r0_k && kend <= r0_end) {
+                    // inside the current linear run: exact c + k*delta, no walking, no test
+                    v.c = r0_base + (float)(v.k0 - r0_k) * r0_del;
+                    v.del = r0_del;
+                    v.lin = true;
+                } else {
+                    // state = exact value at pixel r0_sk: contiguous chunks need 0 or 1 step
+                    v.c = v.k0 == r0_sk ? r0_sc
+                                        : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
+                    const float j = linear_run(v.c, v.d, &v.del);
+                    v.lin = j >= (float)(v.m - 1u);
+                    if (j >= 1.0f) {
+                        r0_base = v.c; r0_k = v.k0; r0_del = v.del;
+                        r0_end = j >= 65536.0f ? 0xFFFFFFFFu : v.k0 + (uint32_t)j;
+                    } else {
+                        r0_k = 1u; r0_end = 0u;
+                    }
+                }
+                if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;   // monotone walk
+            }
+            BatchMasks bm;
+            float last;
+            batch_resolve(v, tl, lane, sh.tab[wave], bm, last S3R_IT(p_chunk));
+            if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
+            if (bm.ovm) {
+#ifdef S3R_STATS
+                st_batches++;
+                st_irr += (v.ov && !v.lin) ? 1u : 0u;
+#endif
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 4)
+                if (x == 0xFFFFFFFFu) win = (int)(bm.ovm ^ bm.negm);   // keep the phase alive, skip pixels
+#else
+                pixel_phase(v, bm, x, sh.tab[wave], depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
+#endif
+            }
+        }
+
         uint32_t cursor = 0, cnt = n0;
         for (;;) {
             if (overflow) {
@@ -507,109 +747,44 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
                 cnt = sh.cnt;
                 cursor = sh.next;
             }
-            for (uint32_t b = 0; row_ok && b * kTPB < cnt; b++) {
+            for (uint32_t b = reg0 ? 1u : 0u; row_ok && b * kTPB < cnt; b++) {
                 const bool stateful = !overflow && b < kStateBatches;
                 // ---- lanes as (triangle, component): advance the exact walk to this chunk
                 const uint32_t idx = b * kTPB + tl;
-                bool ov = false, lin = false, neg = false;
-                float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f;
-                uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
+                BatchLanes v;
                 if (lane < 63 && idx < cnt) {
                     const Entry &e = sh.ent[idx];
-                    ov = y >= e.ymin && y <= e.ymax && e.xmin <= cx1 && e.xmax >= cx0;
-                    if (ov) {
-                        d = e.dx[comp];
-                        rz = e.rvz[comp];
-                        xmax = e.xmax;
-                        slot = e.slot;
-                        k0 = max(cx0, e.xmin);
-                        m = min(cx1, e.xmax) - k0 + 1u;
+                    v.ov = y >= e.ymin && y <= e.ymax && e.xmin <= cx1 && e.xmax >= cx0;
+                    if (v.ov) {
+                        v.d = e.dx[comp];
+                        v.rz = e.rvz[comp];
+                        v.xmax = e.xmax;
+                        v.slot = e.slot;
+                        v.k0 = max(cx0, e.xmin);
+                        v.m = min(cx1, e.xmax) - v.k0 + 1u;
                         if (stateful) {
-                            // state = exact value at pixel kp (xmin or the segment start, or the last
-                            // pixel of the previous chunk): contiguous chunks need 0 or 1 step
                             const uint32_t kp = st_k[b * 64 + lane];
                             const float cp = st_c[b * 64 + lane];
-                            c = k0 == kp ? cp : (k0 == kp + 1u ? cp + d : walk(cp, d, k0 - kp S3R_IT(p_chunk)));
+                            v.c = v.k0 == kp ? cp : (v.k0 == kp + 1u ? cp + v.d : walk(cp, v.d, v.k0 - kp S3R_IT(p_chunk)));
                         } else {
                             const bool inside = e.xmin >= xs;
                             const float c0v = rowtab[(((size_t)e.slot * H + y) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
-                            c = walk(c0v, d, k0 - (inside ? e.xmin : xs) S3R_IT(p_chunk));
+                            v.c = walk(c0v, v.d, v.k0 - (inside ? e.xmin : xs) S3R_IT(p_chunk));
                         }
-                        lin = chunk_linear(c, d, m, &del);
-                        if (lin) neg = c < 0.0f && c + (float)(m - 1u) * del < 0.0f;   // monotone walk
+                        v.lin = chunk_linear(v.c, v.d, v.m, &v.del);
+                        if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;
                     }
                 }
-                const uint64_t ovm = __ballot(ov && comp == 0);
-                if (ovm == 0) continue;
-                // a triangle with one component negative over the whole chunk covers none of it
-                uint64_t negm = __ballot(neg);
-                const uint64_t irrm = __ballot(ov && !lin && !((negm >> (3u * tl)) & 7ull));
-                uint32_t tix = kNoTable;
-                float last = c + (float)(m - 1u) * del;
-                if (ov && !lin) {
-                    if ((negm >> (3u * tl)) & 7ull) {
-                        last = c;                       // pruned: keep the state at the chunk start
-                        m = 1u;
-                    } else {
-                        const uint32_t r = lane_prefix(irrm, lane);
-                        if (r < kTables) {
-                            // the reference's own loop: m - 1 sequential float adds (render.cpp:374)
-                            float v = c;
-                            float *tb = sh.tab[wave][r];
-                            tb[0] = v;
-                            for (uint32_t k = 1; k < m; k++) { v = v + d; tb[k] = v; }
-                            last = v;
-                            tix = r;
-                        } else {
-                            last = walk(c, d, m - 1u S3R_IT(p_chunk));
-                        }
-                        neg = c < 0.0f && last < 0.0f;
-                    }
-                }
-                negm = __ballot(neg);
-                if (ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = k0 + m - 1u; }
-                if (irrm) wave_sync();
+                BatchMasks bm;
+                float last;
+                batch_resolve(v, tl, lane, sh.tab[wave], bm, last S3R_IT(p_chunk));
+                if (v.ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = v.k0 + v.m - 1u; }
+                if (bm.ovm == 0) continue;
 #ifdef S3R_STATS
                 st_batches++;
-                st_irr += (ov && !lin) ? 1u : 0u;
+                st_irr += (v.ov && !v.lin) ? 1u : 0u;
 #endif
-                // ---- lanes as pixels: triangles in slot order (bit 3t of `live`); the (triangle,
-                // component) values are broadcast from their lanes with v_readlane
-                const uint64_t neg3 = negm | (negm >> 1) | (negm >> 2);
-                uint64_t live = ovm & ~neg3 & 0x9249249249249249ull;   // bits 0, 3, 6, ...
-                while (live) {
-                    const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
-                    live &= live - 1;
-                    const uint32_t tk0 = rdl(k0, l0), txmax = rdl(xmax, l0);
-                    if (x < tk0 || x > txmax) continue;
-#ifdef S3R_STATS
-                    st_tests++;
-#endif
-                    const uint32_t off = x - tk0;
-                    const float fo = (float)off;
-                    float a[3], r[3];
-#pragma unroll
-                    for (uint32_t cc = 0; cc < 3; cc++) {
-                        const uint32_t l = l0 + cc;
-                        const float cv = rdl(c, l), dv = rdl(del, l);
-                        const uint32_t ti = rdl(tix, l);
-                        r[cc] = rdl(rz, l);
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
-                        a[cc] = cv + fo * dv;
-#else
-                        if (ti != kNoTable) a[cc] = sh.tab[wave][ti][off];
-                        else if (!((irrm >> l) & 1ull)) a[cc] = cv + fo * dv;
-                        else a[cc] = walk(cv, rdl(d, l), off S3R_IT(p_pix));
-#endif
-                    }
-                    if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
-                        const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
-                        if (ooz > depth) {                                              // :364
-                            depth = ooz; win = (int)rdl(slot, l0); bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
-                        }
-                    }
-                }
-                if (irrm) wave_sync();
+                pixel_phase(v, bm, x, sh.tab[wave], depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
             }
             if (!overflow || cursor >= nslots) break;
         }
@@ -690,14 +865,27 @@ void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t
                            tris, H, segs, 64u * kSegChunks, rowtab);
 }
 
+uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
+    return (uint64_t)((rows_local + kWaves - 1) / kWaves) * fragment_segments(W);
+}
+size_t bin_entry_bytes() { return sizeof(Entry) * kListMax; }
+
+void launch_bin(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
+                uint32_t part, uint32_t rows_local, void *bins, uint32_t *counts, hipStream_t st) {
+    const uint64_t nb = fragment_bins(W, rows_local);
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_bin, dim3((uint32_t)((nb + 3) / 4)), dim3(256), 0, st, tris, nslots, W, H, band, nparts, part,
+                       rows_local, fragment_segments(W), 64u * kSegChunks, (Entry *)bins, counts);
+}
+
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, hipStream_t st) {
-    const uint32_t segs = (W + 64u * kSegChunks - 1) / (64u * kSegChunks);
-    const uint64_t blocks = (uint64_t)((rows_local + kWaves - 1) / kWaves) * segs;
+                     uint32_t rows_local, const void *bins, const uint32_t *counts, hipStream_t st) {
+    const uint32_t segs = fragment_segments(W);
+    const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_fragment<kSegChunks>, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab,
-                       tex, ntex, out, W, H, band, nparts, part, segs, rows_local);
+                       tex, ntex, out, W, H, band, nparts, part, segs, rows_local, (const Entry *)bins, counts);
 }
 
 }  // namespace s3r

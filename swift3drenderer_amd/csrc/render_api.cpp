@@ -60,6 +60,9 @@ struct Lib {
     TriSetup *tris[2] = {nullptr, nullptr};
     float *rowtab[2] = {nullptr, nullptr};     // 2T x H x (segments + 1) x float4 exact row starts
     size_t rowtab_cap = 0;
+    void *bins[2] = {nullptr, nullptr};        // per-workgroup triangle lists (k_bin)
+    uint32_t *bin_counts[2] = {nullptr, nullptr};
+    uint64_t bins_cap = 0;
     hipEvent_t geo_done[2] = {nullptr, nullptr}, frag_done[2] = {nullptr, nullptr};
     uint32_t parity = 0;
     uint32_t *frame = nullptr;
@@ -242,7 +245,7 @@ void release_all() {
         (void)hipDeviceSynchronize();
         unregister_all();
         void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.tris[0], g.tris[1], g.frame,
-                        g.rowtab[0], g.rowtab[1]};
+                        g.rowtab[0], g.rowtab[1], g.bins[0], g.bins[1], g.bin_counts[0], g.bin_counts[1]};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
         for (int p = 0; p < 2; p++) {
@@ -304,18 +307,31 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
         }
         g.rowtab_cap = need;
     }
+    const uint64_t nbins = fragment_bins(W, rows_local);
+    if (g.bins_cap < nbins) {
+        HIPCHECK(hipDeviceSynchronize());
+        for (int p = 0; p < 2; p++) {
+            if (g.bins[p]) HIPCHECK(hipFree(g.bins[p]));
+            if (g.bin_counts[p]) HIPCHECK(hipFree(g.bin_counts[p]));
+            g.bins[p] = dalloc<uint8_t>(nbins * bin_entry_bytes());
+            g.bin_counts[p] = dalloc<uint32_t>(nbins);
+        }
+        g.bins_cap = nbins;
+    }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
     const uint32_t p = g.parity;
     g.parity ^= 1u;
     HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
     launch_setup(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh, g.tris[p], g.geo);
+    launch_bin(g.tris[p], 2 * g.ntri, W, H, band, nparts, part, rows_local, g.bins[p], g.bin_counts[p], g.geo);
     launch_rowstart(g.tris[p], 2 * g.ntri, W, H, g.rowtab[p], g.geo);
     HIPCHECK(hipEventRecord(g.geo_done[p], g.geo));
     // fragment on the caller's stream
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local, st);
+    launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
+                    g.bins[p], g.bin_counts[p], st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(g.frag_done[p], st));
     HIPCHECK(hipGetLastError());

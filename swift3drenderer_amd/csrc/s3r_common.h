@@ -112,6 +112,25 @@ S3R_HD float exact_walk(float s, float d, uint32_t n, uint32_t *iters = nullptr)
     return s;
 }
 
+// Length of the linear run starting at c: the largest j such that S(c, d, k) == c + k*delta for
+// every k <= j (0: not even one regular step; +inf: the walk has stagnated, delta == 0).
+S3R_HD float linear_run(float c, float d, float *delta) {
+    *delta = 0.0f;
+    const float ad = fabsf(d);
+    if (!is_finite(c) || !is_finite(d)) return 0.0f;
+    if (ad == 0.0f) return c != 0.0f ? __builtin_inff() : 0.0f;   // c + 0 == c unless c is -0
+    const float ac = fabsf(c);
+    const bool towards_zero = (c < 0.0f) != (d < 0.0f);
+    const float s1 = c + d, s2 = s1 + d;
+    const uint32_t e = fexp(c);
+    const float del = s1 - c;
+    const bool steady = (ac >= 4.0f * ad) & !(towards_zero & (ac < 8.0f * ad)) & (e >= 32u) & (e < 254u) &
+                        (fexp(s1) == e) & (fexp(s2) == e) & (del == s2 - s1);
+    *delta = steady ? del : 0.0f;
+    const float j = del == 0.0f ? __builtin_inff() : regular_steps(c, d, del, e);
+    return steady ? j : 0.0f;
+}
+
 // True when the m values S(c, d, k), k = 0..m-1, are exactly c + k*delta (one binade, constant
 // step); *delta receives the step.  This is exact_walk's jump test applied to a chunk of m pixels.
 S3R_HD bool chunk_linear(float c, float d, uint32_t m, float *delta) {

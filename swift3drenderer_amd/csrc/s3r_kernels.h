@@ -13,7 +13,14 @@ void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, hipStream_t st);
+                     uint32_t rows_local, const void *bins, const uint32_t *counts, hipStream_t st);
+
+// Per-workgroup triangle lists (bins = row blocks x segments): fragment_bins() bins of
+// bin_entry_bytes() each plus one u32 count per bin.
+uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
+size_t bin_entry_bytes();
+void launch_bin(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
+                uint32_t part, uint32_t rows_local, void *bins, uint32_t *counts, hipStream_t st);
 
 // rowtab (nslots x H x (segments + 1) x float4): exact barycentrics of every live slot's bbox rows at
 // x = xmin and at each fragment-segment boundary inside the bbox.

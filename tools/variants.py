@@ -10,9 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
-    'seg4': {'S3R_SEG_CHUNKS': 4},
-    'seg6': {'S3R_SEG_CHUNKS': 6},
-    'seg8': {'S3R_SEG_CHUNKS': 8},
+    'occ5': {'S3R_OCC': 5},
+    'occ6': {'S3R_OCC': 6},
+    'occ4': {'S3R_OCC': 4},
 }
 
 
