@@ -91,11 +91,23 @@ def build_data(force: bool = False) -> str:
     return DATA
 
 
+HOST_SRC = os.path.join(ROOT, 'host', 'main_loop.cpp')
+HOST_BIN = os.path.join(ROOT, 'host', 'main_loop')
+
+
+def build_host(force: bool = False) -> str:
+    """The C++ counterpart of main.swift's loop (dlopen + per-frame updateAndRender); plain g++."""
+    if force or not _newer(HOST_BIN, [HOST_SRC, os.path.join(ROOT, 'include', 'render.h')]):
+        subprocess.run(['g++', '-O2', '-std=c++17', '-Wall', HOST_SRC, '-ldl', '-o', HOST_BIN], check=True)
+    return HOST_BIN
+
+
 def main():
     build_library(force='--force' in sys.argv, verbose=True)
     if '--stats' in sys.argv:
         build_library(force='--force' in sys.argv, verbose=True, stats=True)
     build_data()
+    build_host()
     print(LIB)
 
 

@@ -285,7 +285,10 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint
 
 // ------------------------------------------------------------------ K4: fragment
 constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + component (63 lanes)
-constexpr uint32_t kWaves = 4;         // one wave per row: a workgroup is 4 consecutive local rows
+#ifndef S3R_WAVES
+#define S3R_WAVES 4
+#endif
+constexpr uint32_t kWaves = S3R_WAVES; // one wave per row: a workgroup is kWaves consecutive local rows
 constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
 #ifndef S3R_STATE_BATCHES
 #define S3R_STATE_BATCHES 4
@@ -296,6 +299,11 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #ifndef S3R_OCC
 #define S3R_OCC 5                      // target waves per SIMD (5: no spills at <= 96 VGPRs)
 #endif
+#ifndef S3R_PX
+#define S3R_PX 1
+#endif
+constexpr uint32_t kPX = S3R_PX;       // pixels per lane: a chunk is 64 * kPX consecutive pixels of a row
+constexpr uint32_t kChunk = 64u * kPX;
 constexpr uint32_t kStateBatches = S3R_STATE_BATCHES;  // batches whose walk state persists in LDS
 constexpr uint32_t kTables = S3R_TABLES;  // per wave: 64-entry exact-value tables, non-linear chunks
 
@@ -312,7 +320,7 @@ struct FragShared {
     uint32_t cnt, next;
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
-    float tab[kWaves][kTables][64];      // exact S(c, d, k), k = 0..63, filled by sequential adds
+    float tab[kWaves][kTables][kChunk];  // exact S(c, d, k), k < kChunk, filled by sequential adds
 };
 constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
@@ -335,8 +343,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#if defined(S3R_INLINE) && S3R_INLINE
+#define S3R_CALLEE __device__ __forceinline__
+#else
+#define S3R_CALLEE __device__ __noinline__
+#endif
 // Out-of-line walker: one copy of the loop for every call site (code size, i-cache).
-__device__ __noinline__ float walk(float s, float d, uint32_t n
+S3R_CALLEE float walk(float s, float d, uint32_t n
 #ifdef S3R_STATS
                                    , uint32_t *iters
 #endif
@@ -452,7 +465,7 @@ __global__ void __launch_bounds__(256) k_bin(const TriSetup *__restrict__ tris, 
 }
 
 // Deferred shading of the winning triangle (render.cpp:366-371).
-__device__ __noinline__ uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
+S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
                                        const uint32_t *__restrict__ tex, uint32_t ntex) {
     const float4 *q = reinterpret_cast<const float4 *>(tp);
     const uint4 hdr = reinterpret_cast<const uint4 *>(tp)[0];
@@ -502,7 +515,7 @@ struct BatchMasks {
 // covers none of it; a non-linear component gets a 64-entry table filled by the reference's own
 // sequential loop (render.cpp:374).  `last` = the component's exact value at the chunk's last pixel
 // (or at its first, for a pruned non-linear component), the walk state for the next chunk.
-__device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32_t lane, float (*tab)[64],
+__device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32_t lane, float (*tab)[kChunk],
                                               BatchMasks &bm, float &last
 #ifdef S3R_STATS
                                               , uint32_t *p_chunk
@@ -539,8 +552,9 @@ __device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32
 
 // Lanes as pixels: triangles in slot order (bit 3t of `live`); (triangle, component) values are
 // broadcast from their lanes with v_readlane.  Edge test, 1/z, strict '>' depth test in registers.
-__device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMasks &bm, uint32_t x, float (*tab)[64],
-                                            float &depth, int &win, float &bw0, float &bw1, float &bw2
+__device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMasks &bm, uint32_t xl, float (*tab)[kChunk],
+                                            float (&depth)[kPX], int (&win)[kPX], float (&bw0)[kPX],
+                                            float (&bw1)[kPX], float (&bw2)[kPX]
 #ifdef S3R_STATS
                                             , uint32_t *p_pix, uint32_t *p_tests
 #endif
@@ -551,33 +565,46 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
         const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
         live &= live - 1;
         const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0);
-        if (x < tk0 || x > txmax) continue;
-#ifdef S3R_STATS
-        (*p_tests)++;
-#endif
-        const uint32_t off = x - tk0;
-        const float fo = (float)off;
-        float a[3], r[3];
+        float cv[3], dv[3], r[3];
+        uint32_t lmask = 0;
 #pragma unroll
         for (uint32_t cc = 0; cc < 3; cc++) {
             const uint32_t l = l0 + cc;
-            const float cv = rdl(v.c, l), dv = rdl(v.del, l);
+            cv[cc] = rdl(v.c, l);
+            dv[cc] = rdl(v.del, l);
             r[cc] = rdl(v.rz, l);
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
-            a[cc] = cv + fo * dv;
-#else
-            if (!((bm.irrm >> l) & 1ull)) {
-                a[cc] = cv + fo * dv;                          // linear chunk (or pruned: unused)
-            } else {
-                const uint32_t ti = rdl(bm.tix, l);
-                a[cc] = ti != kNoTable ? tab[ti][off] : walk(cv, rdl(v.d, l), off S3R_IT(p_pix));
-            }
-#endif
+            lmask |= (uint32_t)((bm.irrm >> l) & 1ull) << cc;
         }
-        if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
-            const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
-            if (ooz > depth) {                                              // :364
-                depth = ooz; win = (int)rdl(v.slot, l0); bw0 = a[0]; bw1 = a[1]; bw2 = a[2];
+        const int tslot = (int)rdl(v.slot, l0);
+#pragma unroll
+        for (uint32_t p = 0; p < kPX; p++) {
+            const uint32_t x = xl + 64u * p;
+            if (x < tk0 || x > txmax) continue;
+#ifdef S3R_STATS
+            (*p_tests)++;
+#endif
+            const uint32_t off = x - tk0;
+            const float fo = (float)off;
+            float a[3];
+#pragma unroll
+            for (uint32_t cc = 0; cc < 3; cc++) {
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
+                a[cc] = cv[cc] + fo * dv[cc];
+#else
+                if (!((lmask >> cc) & 1u)) {
+                    a[cc] = cv[cc] + fo * dv[cc];                      // linear chunk (or pruned: unused)
+                } else {
+                    const uint32_t l = l0 + cc;
+                    const uint32_t ti = rdl(bm.tix, l);
+                    a[cc] = ti != kNoTable ? tab[ti][off] : walk(cv[cc], rdl(v.d, l), off S3R_IT(p_pix));
+                }
+#endif
+            }
+            if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
+                const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
+                if (ooz > depth[p]) {                                           // :364
+                    depth[p] = ooz; win[p] = tslot; bw0[p] = a[0]; bw1[p] = a[1]; bw2[p] = a[2];
+                }
             }
         }
     }
@@ -590,7 +617,7 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 // that component's exact walk (render.cpp:374) to the chunk, publishing (value, step) in LDS; then
 // its lanes act as pixels: edge test, 1/z, strict '>' depth test in registers; the winner is shaded.
 template <uint32_t SEGCH>
-__global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
+__global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
@@ -609,8 +636,8 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
         const uint32_t yy = row_of(lr0 + k);
         y0 = min(y0, yy); y1 = max(y1, yy);
     }
-    const uint32_t xs = seg * 64u * SEGCH;
-    const uint32_t xe = min(W, xs + 64u * SEGCH) - 1u;
+    const uint32_t xs = seg * kChunk * SEGCH;
+    const uint32_t xe = min(W, xs + kChunk * SEGCH) - 1u;
     const uint32_t tl = lane / 3u, comp = lane - 3u * tl;                  // (triangle, component) role
     float *st_c = sh.st_c[wave];
     uint32_t *st_k = sh.st_k[wave];
@@ -684,12 +711,14 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
 
     uint32_t *row = out + (size_t)lr * W;
     for (uint32_t q = 0; q < SEGCH; q++) {
-        const uint32_t cx0 = xs + 64u * q;
+        const uint32_t cx0 = xs + kChunk * q;
         if (cx0 > xe) break;
-        const uint32_t cx1 = min(cx0 + 63u, xe);
-        const uint32_t x = cx0 + lane;
-        float depth = 0.0f, bw0 = 0.0f, bw1 = 0.0f, bw2 = 0.0f;
-        int win = -1;
+        const uint32_t cx1 = min(cx0 + kChunk - 1u, xe);
+        const uint32_t x = cx0 + lane;                     // this lane's pixels: x + 64 p, p < kPX
+        float depth[kPX], bw0[kPX], bw1[kPX], bw2[kPX];
+        int win[kPX];
+#pragma unroll
+        for (uint32_t p = 0; p < kPX; p++) { depth[p] = 0.0f; bw0[p] = bw1[p] = bw2[p] = 0.0f; win[p] = -1; }
 
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 8)
         if (false) {
@@ -733,7 +762,7 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
                 st_irr += (v.ov && !v.lin) ? 1u : 0u;
 #endif
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 4)
-                if (x == 0xFFFFFFFFu) win = (int)(bm.ovm ^ bm.negm);   // keep the phase alive, skip pixels
+                if (x == 0xFFFFFFFFu) win[0] = (int)(bm.ovm ^ bm.negm);   // keep the phase alive, skip pixels
 #else
                 pixel_phase(v, bm, x, sh.tab[wave], depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
 #endif
@@ -788,11 +817,19 @@ __global__ void __launch_bounds__(256, S3R_OCC) k_fragment(const TriSetup *__res
             }
             if (!overflow || cursor >= nslots) break;
         }
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 1)
-        if (row_ok && x <= xe) row[x] = win < 0 ? kBackground : (uint32_t)win ^ __float_as_uint(bw0 + bw1 + bw2 + depth);
+#pragma unroll
+        for (uint32_t p = 0; p < kPX; p++) {
+            const uint32_t xp = x + 64u * p;
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 128)
+            if (row_ok && xp <= xe && win[p] == 12345) row[xp] = 0;    // ablation: no stores
+#elif defined(S3R_ABLATE) && (S3R_ABLATE & 1)
+            if (row_ok && xp <= xe)
+                row[xp] = win[p] < 0 ? kBackground : (uint32_t)win[p] ^ __float_as_uint(bw0[p] + bw1[p] + bw2[p] + depth[p]);
 #else
-        if (row_ok && x <= xe) row[x] = win < 0 ? kBackground : shade(tris + win, bw0, bw1, bw2, depth, tex, ntex);
+            if (row_ok && xp <= xe)
+                row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #endif
+        }
     }
 #ifdef S3R_STATS
     {
@@ -839,10 +876,11 @@ void stats_read(unsigned long long out[16], bool reset) {
 }
 
 // ------------------------------------------------------------------ launchers
-#ifndef S3R_SEG_CHUNKS
-#define S3R_SEG_CHUNKS 6
+#ifndef S3R_SEG_PIXELS
+#define S3R_SEG_PIXELS 384
 #endif
-constexpr uint32_t kSegChunks = S3R_SEG_CHUNKS;   // 64-pixel chunks per fragment segment
+constexpr uint32_t kSegChunks = S3R_SEG_PIXELS / kChunk;   // chunks per fragment segment
+static_assert(kSegChunks * kChunk == S3R_SEG_PIXELS, "segment = whole chunks");
 
 void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                   const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
@@ -852,9 +890,9 @@ void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const
                        m, factor, sw, sh, tris);
 }
 
-uint32_t fragment_segment_pixels() { return 64u * kSegChunks; }
+uint32_t fragment_segment_pixels() { return kChunk * kSegChunks; }
 
-uint32_t fragment_segments(uint32_t W) { return (W + 64u * kSegChunks - 1) / (64u * kSegChunks); }
+uint32_t fragment_segments(uint32_t W) { return (W + kChunk * kSegChunks - 1) / (kChunk * kSegChunks); }
 
 void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st) {
     if (nslots == 0 || H == 0) return;
@@ -862,7 +900,7 @@ void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t
     hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, segs, rowtab);
     if (segs > 1)
         hipLaunchKernelGGL(k_segstart, dim3(nslots, (H + 63) / 64, 3 * ((segs - 1 + 3) / 4)), dim3(64, 4), 0, st,
-                           tris, H, segs, 64u * kSegChunks, rowtab);
+                           tris, H, segs, kChunk * kSegChunks, rowtab);
 }
 
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
@@ -875,7 +913,7 @@ void launch_bin(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, u
     const uint64_t nb = fragment_bins(W, rows_local);
     if (nb == 0) return;
     hipLaunchKernelGGL(k_bin, dim3((uint32_t)((nb + 3) / 4)), dim3(256), 0, st, tris, nslots, W, H, band, nparts, part,
-                       rows_local, fragment_segments(W), 64u * kSegChunks, (Entry *)bins, counts);
+                       rows_local, fragment_segments(W), kChunk * kSegChunks, (Entry *)bins, counts);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

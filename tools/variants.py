@@ -10,9 +10,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
-    'occ5': {'S3R_OCC': 5},
-    'occ6': {'S3R_OCC': 6},
-    'occ4': {'S3R_OCC': 4},
+    'calls': {'S3R_INLINE': 0},
+    'inline': {'S3R_INLINE': 1},
+    'inline_skel': {'S3R_INLINE': 1, 'S3R_ABLATE': 189},
+    'calls_skel': {'S3R_INLINE': 0, 'S3R_ABLATE': 189},
 }
 
 
