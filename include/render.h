@@ -54,6 +54,16 @@ int s3r_configure(const char *data_path, int device);
 /* Release every GPU resource and registered host buffer; the next call re-initialises. */
 void s3r_shutdown(void);
 
+/* Fragment-stage strategy (extension; both are bit-identical to render.cpp):
+ *   1 = row path: per-(slot, row) exact start table + per-workgroup triangle lists, lanes as
+ *       (triangle, component) then as pixels -- for the packaged-size scenes;
+ *   2 = tile path: order-independent 16x64-pixel tiles, per-pixel (1/z, slot) max in LDS, then
+ *       deferred shading -- for many triangles (the icosahedron stress scene);
+ *   0 = automatic (default): tile path above 8192 triangle slots (2 x triangles).
+ * Returns 0, or -1 for an unknown mode.  s3r_raster_path() reports the path the next frame takes. */
+int s3r_set_raster_path(int mode);
+int s3r_raster_path(void);
+
 /* One frame for one part of an interleaved row-band split (multi-GPU).  Same camera / init /
  * resize semantics as updateAndRender.  Frame row y belongs to part ((y / band_rows) % n_parts);
  * this part's rows are written compactly, in increasing y, to the DEVICE buffer dev_out

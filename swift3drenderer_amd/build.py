@@ -24,7 +24,7 @@ ARCH = os.environ.get('S3R_ARCH', 'gfx950')
 # -ffp-contract=off: no FMA contraction (bit parity with the x86 reference build); no fast-math:
 # IEEE-correct division and sqrt.
 FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-ffp-contract=off',
-         '-fno-fast-math', '-Wall', '-Wno-unused-function', f'-I{os.path.join(ROOT, "include")}']
+         '-fno-fast-math', '-Wall', '-Wno-unused-function', '-Wno-bitwise-instead-of-logical', f'-I{os.path.join(ROOT, "include")}']
 SOURCES = ['kernels.hip', 'render_api.cpp']
 
 

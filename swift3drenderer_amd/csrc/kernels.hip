@@ -100,20 +100,15 @@ __device__ __forceinline__ float edge_fn(F3 a, F3 b, float cx, float cy) {
     return (cx - a.x) * (a.y - b.y) + (cy - a.y) * (b.x - a.x);     // EDGE_FUNCTION, render.cpp:9
 }
 
-// render.cpp:311-359 for one (possibly clipped) triangle.
-__device__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, TriSetup *out) {
-    TriSetup t;
-    t.kind = kDead;
-    t.pad0 = t.pad1 = 0;
+// render.cpp:311-336, the position-only part of the setup: reject / cull (:312, :314, :317), bbox,
+// wstart, per-pixel and per-row steps, 1/z per corner.  False = no pixel of the frame.
+__device__ __forceinline__ bool raster_part(const Vert d[3], float sw, float sh, TriSetup &t) {
     const float rmx = fmaxf(fmaxf(d[0].rv.x, d[1].rv.x), d[2].rv.x);
     const float rmy = fmaxf(fmaxf(d[0].rv.y, d[1].rv.y), d[2].rv.y);
     const float rnx = fminf(fminf(d[0].rv.x, d[1].rv.x), d[2].rv.x);
     const float rny = fminf(fminf(d[0].rv.y, d[1].rv.y), d[2].rv.y);
     const float area = edge_fn(d[0].rv, d[1].rv, d[2].rv.x, d[2].rv.y);
-    if (rmx < 0 || rmy < 0 || rnx >= sw || rny >= sh || area < 10) {   // :312, :314, :317
-        out->kind = kDead;
-        return;
-    }
+    if (rmx < 0 || rmy < 0 || rnx >= sw || rny >= sh || area < 10) return false;   // :312, :314, :317
     const float ooa = 1 / area;
     t.xmin = u32_of_float(fmaxf(0, rnx));
     t.xmax = u32_of_float(fminf(sw - 1, rmx));
@@ -131,9 +126,22 @@ __device__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, Tr
     t.dy[2] = (d[1].rv.x - d[0].rv.x) * ooa;
     t.ws[3] = t.dx[3] = t.dy[3] = t.rvz[3] = 0.0f;
 #pragma unroll
+    for (int k = 0; k < 3; k++) t.rvz[k] = 1 / d[k].rv.z;
+    return true;
+}
+
+// render.cpp:311-359 for one (possibly clipped) triangle.
+__device__ __forceinline__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, TriSetup *out) {
+    TriSetup t;
+    t.kind = kDead;
+    t.pad0 = t.pad1 = 0;
+    if (!raster_part(d, sw, sh, t)) {
+        out->kind = kDead;
+        return;
+    }
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-        const float r = 1 / d[k].rv.z;
-        t.rvz[k] = r;
+        const float r = t.rvz[k];
         t.cvr[4 * k + 0] = d[k].cv.x * r; t.cvr[4 * k + 1] = d[k].cv.y * r; t.cvr[4 * k + 2] = d[k].cv.z * r;
         t.nr[4 * k + 0] = d[k].n.x * r; t.nr[4 * k + 1] = d[k].n.y * r; t.nr[4 * k + 2] = d[k].n.z * r;
         t.cvr[4 * k + 3] = t.nr[4 * k + 3] = 0.0f;
@@ -343,12 +351,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#if defined(S3R_INLINE) && S3R_INLINE
+// Walker and shader inlined (default): no call frame, no scratch stack (measured 72.6 vs 75.1 us per
+// 4K P_over launch against the out-of-line build, S3R_INLINE=0).
+#ifndef S3R_INLINE
+#define S3R_INLINE 1
+#endif
+#if S3R_INLINE
 #define S3R_CALLEE __device__ __forceinline__
 #else
 #define S3R_CALLEE __device__ __noinline__
 #endif
-// Out-of-line walker: one copy of the loop for every call site (code size, i-cache).
 S3R_CALLEE float walk(float s, float d, uint32_t n
 #ifdef S3R_STATS
                                    , uint32_t *iters
@@ -843,6 +855,361 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
 #endif
 }
 
+// ------------------------------------------------------------------ tile path (many triangles)
+// For scenes whose slot count makes the per-(slot, row) start table too large (the icosahedron
+// stress scene, BASELINE config 5: 20 M triangles), the fragment stage is order-independent:
+//   k_tile_setup   one thread per triangle, POSITIONS ONLY (vertex transform, reject, near clip,
+//                  cull, raster setup; render.cpp:285-336): a 64-B RasterRec per live slot, a packed
+//                  bbox word per triangle, and the per-tile counts (wave-aggregated atomics);
+//   k_tile_scan    exclusive scan of the counts;   k_tile_fill  scatter slot ids into tile lists;
+//   k_tile_raster  one workgroup per tile of 16 local rows x 64 px: lanes take (triangle, row)
+//                  items and walk the row with the reference's own sequential adds (render.cpp:374,
+//                  :378; row start by exact_walk), keeping per pixel the max of
+//                  key = (bits(1/z) << 32) | ~slot in LDS (ds_max_u64).  Strict '>' on 1/z from 0.0
+//                  (:364) keeps the first of the deepest fragments in slot order, i.e. the largest
+//                  1/z with ties to the smallest slot = the max key (1/z > 0 orders as its bits).
+//                  Each pixel's winner is then re-walked exactly and shaded; its shading constants
+//                  (normals, colours / uvs: the attribute stream) are recomputed from the scene by the
+//                  same setup code, so attributes are read only for visible triangles.
+constexpr uint32_t kTileW = 64, kTileH = 16, kTileThreads = 256, kTileStage = 256;
+constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of one column hit different banks
+constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
+
+struct alignas(16) RasterRec {                     // 64 B: one line per live slot
+    uint32_t bx, by, slot, pad;                    // bx = xmin | xmax << 16, by = ymin | ymax << 16
+    float ws[3], dx0;
+    float dx12[2], dy01[2];
+    float dy2, rz[3];
+};
+static_assert(sizeof(RasterRec) == 64, "RasterRec layout");
+
+__device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint32_t vi, const Mat34 &m, float factor,
+                                            float half_w, float half_h, Vert &d) {
+    const F3 c = mat_mul(m, vtx[vi]);                                     // :286
+    const float nz = -c.z;
+    d.cv = c;
+    d.rv = mk3((c.x * factor) / nz + half_w, ((-c.y) * factor) / nz + half_h, (0.0f * factor) / nz + nz);   // :288
+}
+
+// Local rows [lo, hi] of this rank that fall in frame rows [ymin, ymax] (interleaved bands: local
+// row order is frame row order, so the owned rows of any frame-row interval are one local range).
+__device__ __forceinline__ bool local_row_range(uint32_t ymin, uint32_t ymax, uint32_t band, uint32_t nparts,
+                                                uint32_t part, uint32_t &lo, uint32_t &hi) {
+    const uint32_t g0 = ymin / band, g1 = ymax / band;
+    uint32_t fg = g0, fy = ymin;
+    if (g0 % nparts != part) { fg = g0 + (part + nparts - g0 % nparts) % nparts; fy = fg * band; }
+    uint32_t lg = g1, ly = ymax;
+    if (g1 % nparts != part) {
+        const uint32_t d = (g1 % nparts + nparts - part) % nparts;
+        if (g1 < d) return false;
+        lg = g1 - d; ly = lg * band + band - 1u;
+    }
+    if (fg > lg || fy > ly) return false;
+    lo = (fg / nparts) * band + (fy - fg * band);
+    hi = (lg / nparts) * band + (ly - lg * band);
+    return true;
+}
+
+struct TileSpan { uint32_t tx0, ntx, ty0, n; };     // tiles tx0 .. tx0+ntx-1 x ty0 .., n in all
+
+__device__ __forceinline__ TileSpan box_tiles(uint32_t bx, uint32_t by, uint32_t band, uint32_t nparts, uint32_t part) {
+    TileSpan sp{0, 1, 0, 0};
+    uint32_t lo, hi;
+    if (bx == kDeadBox || !local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi)) return sp;
+    sp.tx0 = (bx & 0xFFFFu) / kTileW;
+    sp.ntx = (bx >> 16) / kTileW - sp.tx0 + 1u;
+    sp.ty0 = lo / kTileH;
+    sp.n = sp.ntx * (hi / kTileH - sp.ty0 + 1u);
+    return sp;
+}
+
+// Every lane adds 1 to counter[key] for each tile of its span (or nothing); lanes of the wave with
+// the same key share one atomic.  With `list`, the returned positions place `slot` in the lists.
+__device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x, uint32_t *__restrict__ ctr,
+                                           uint32_t *__restrict__ list, uint32_t slot) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t rounds = sp.n;
+    for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
+    for (uint32_t k = 0; k < rounds; k++) {
+        const bool act = k < sp.n;
+        const uint32_t key = act ? (sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx : 0xFFFFFFFFu;
+        uint64_t todo = __ballot(act);
+        while (todo) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
+            const uint64_t grp = __ballot(act && key == lk);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&ctr[lk], (uint32_t)__builtin_popcountll(grp));
+            if (list) {
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+                if (act && key == lk) list[base + lane_prefix(grp, lane)] = slot;
+            }
+            todo &= ~grp;
+        }
+    }
+}
+
+__device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot) {
+    float4 *q = reinterpret_cast<float4 *>(r);
+    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot, 0u);
+    q[1] = make_float4(t.ws[0], t.ws[1], t.ws[2], t.dx[0]);
+    q[2] = make_float4(t.dx[1], t.dx[2], t.dy[0], t.dy[1]);
+    q[3] = make_float4(t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]);
+}
+
+__global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
+                                                    uint32_t ntri, Mat34 m, float factor, float sw, float sh,
+                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
+                                                    RasterRec *__restrict__ recs, uint32_t *__restrict__ boxes,
+                                                    uint32_t *__restrict__ app_list, uint32_t *__restrict__ app_count,
+                                                    uint32_t *__restrict__ counts) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = t < ntri;
+    const float half_w = sw / 2, half_h = sh / 2;
+    Vert d[3];
+    TriSetup ts;
+    bool live = false;
+    if (in) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
+            d[k].n = mk3(0, 0, 0);
+            d[k].pay = make_float4(0, 0, 0, 0);
+        }
+        if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
+            if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear) {               // :308, rare
+                Vert app[3];
+                uint32_t app_first = 0;
+                // positions do not depend on the colour / texture payload (clip's `textured`)
+                if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) {
+                    TriSetup ta;
+                    if (raster_part(app, sw, sh, ta)) {
+                        write_rec(recs + ntri + t, ta, ntri + t);
+                        app_list[atomicAdd(app_count, 1u)] = ntri + t;
+                        const TileSpan sa = box_tiles(ta.xmin | (ta.xmax << 16), ta.ymin | (ta.ymax << 16), band,
+                                                      nparts, part);
+                        for (uint32_t k = 0; k < sa.n; k++)
+                            atomicAdd(&counts[(sa.ty0 + k / sa.ntx) * tiles_x + sa.tx0 + k % sa.ntx], 1u);
+                    }
+                }
+            }
+            live = raster_part(d, sw, sh, ts);
+        }
+    }
+    uint32_t bx = kDeadBox, by = 0;
+    if (live) {
+        bx = ts.xmin | (ts.xmax << 16);
+        by = ts.ymin | (ts.ymax << 16);
+        write_rec(recs + t, ts, t);
+    }
+    if (in) reinterpret_cast<uint2 *>(boxes)[t] = make_uint2(bx, by);
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 1)
+    if (bx == 12345u)                                   // ablation: no tile counting
+#endif
+    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, counts, nullptr, 0);
+}
+
+// Exclusive scan of the tile counts (one workgroup): offs[t], cursor[t] = offs[t], *total.
+__global__ void __launch_bounds__(1024) k_tile_scan(const uint32_t *__restrict__ counts, uint32_t ntiles,
+                                                    uint32_t *__restrict__ offs, uint32_t *__restrict__ cursor,
+                                                    uint32_t *__restrict__ total) {
+    __shared__ uint32_t part_sum[1024];
+    const uint32_t per = (ntiles + 1023u) / 1024u;
+    const uint32_t b = threadIdx.x * per, e = min(ntiles, b + per);
+    uint32_t sum = 0;
+    for (uint32_t i = b; i < e; i++) sum += counts[i];
+    part_sum[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024u; o <<= 1) {          // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= o ? part_sum[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part_sum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part_sum[threadIdx.x] - sum;
+    for (uint32_t i = b; i < e; i++) { offs[i] = run; cursor[i] = run; run += counts[i]; }
+    if (threadIdx.x == 1023u) *total = part_sum[1023];
+}
+
+// Scatter: threads [0, ntri) the original triangles (packed bboxes), then the clip-appended slots.
+__global__ void __launch_bounds__(256) k_tile_fill(const uint32_t *__restrict__ boxes, uint32_t ntri,
+                                                   const RasterRec *__restrict__ recs,
+                                                   const uint32_t *__restrict__ app_list, uint32_t napp,
+                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
+                                                   uint32_t *__restrict__ cursor, uint32_t *__restrict__ list) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t bx = kDeadBox, by = 0, slot = 0;
+    if (i < ntri) {
+        const uint2 b = reinterpret_cast<const uint2 *>(boxes)[i];
+        bx = b.x; by = b.y; slot = i;
+    } else if (i - ntri < napp) {
+        slot = app_list[i - ntri];
+        const uint4 h = reinterpret_cast<const uint4 *>(recs + slot)[0];
+        bx = h.x; by = h.y;
+    }
+    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, slot);
+}
+
+struct TileShared {
+    unsigned long long key[kTileH * kKeyStride];
+    float ws[3][kTileStage], dx[3][kTileStage], dy[3][kTileStage], rz[3][kTileStage];
+    uint32_t slot[kTileStage], xmin[kTileStage], xmax[kTileStage], ymin[kTileStage], r0[kTileStage];
+    uint32_t pre[kTileStage + 1];
+    uint32_t wsum[kTileThreads / 64];
+};
+
+// Shading constants of slot s recomputed from the scene exactly as k_setup computes them.
+__device__ __forceinline__ void slot_setup(uint32_t s, uint32_t ntri, const float4 *__restrict__ vtx,
+                                           const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
+                                           const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx,
+                                           const uint32_t *__restrict__ aidx, const Mat34 &m, float factor, float sw,
+                                           float sh, TriSetup &out) {
+    const uint32_t t = s < ntri ? s : s - ntri;
+    const float half_w = sw / 2, half_h = sh / 2;
+    Vert d[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t ai = aidx[3 * t + k];
+        load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
+        d[k].n = mat_mul(m, nrm[ai]);                                       // :291
+        d[k].pay = pay[ai];
+    }
+    bool textured = disc[aidx[3 * t]] != 0;                                  // :340
+    if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear) {
+        Vert app[3];
+        uint32_t app_first = 0;
+        const bool appended = clip_tri(d, app, &app_first, textured, factor, half_w, half_h);
+        if (s >= ntri && appended) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) d[k] = app[k];
+            textured = disc[aidx[3 * t + app_first]] != 0;
+        }
+    }
+    setup_tri(d, textured, sw, sh, &out);
+}
+
+__global__ void __launch_bounds__(kTileThreads) k_tile_raster(
+    const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+    uint32_t tiles_x, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ counts,
+    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys) {
+    __shared__ TileShared ls;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tile = blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const uint32_t lx0 = tx * kTileW, lx1 = min(W, lx0 + kTileW) - 1u;
+    const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
+    auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
+    for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
+    const uint32_t n = counts[tile], base = offs[tile];
+    for (uint32_t c0 = 0; c0 < n; c0 += kTileStage) {
+        __syncthreads();                                 // previous stage fully consumed
+        const uint32_t j = c0 + tid;
+        uint32_t nr = 0;
+        if (j < n) {
+            const uint32_t s = list[base + j];
+            const float4 *q = reinterpret_cast<const float4 *>(recs + s);
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            const uint32_t bx = f2u(q0.x), by = f2u(q0.y);
+            uint32_t lo = 1u, hi = 0u;
+            local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi);
+            const uint32_t a = max(lo, tr0), b = min(hi, tr1);
+            nr = (lo <= hi && a <= b) ? b - a + 1u : 0u;
+            ls.slot[tid] = s; ls.xmin[tid] = bx & 0xFFFFu; ls.xmax[tid] = bx >> 16; ls.ymin[tid] = by & 0xFFFFu;
+            ls.r0[tid] = a;
+            ls.ws[0][tid] = q1.x; ls.ws[1][tid] = q1.y; ls.ws[2][tid] = q1.z;
+            ls.dx[0][tid] = q1.w; ls.dx[1][tid] = q2.x; ls.dx[2][tid] = q2.y;
+            ls.dy[0][tid] = q2.z; ls.dy[1][tid] = q2.w; ls.dy[2][tid] = q3.x;
+            ls.rz[0][tid] = q3.y; ls.rz[1][tid] = q3.z; ls.rz[2][tid] = q3.w;
+        }
+        // exclusive scan of the row counts over the stage (wave shuffles + wave totals)
+        uint32_t inc = nr;
+        for (uint32_t o = 1; o < 64u; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63u) ls.wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (uint32_t w = 0; w < wave; w++) wbase += ls.wsum[w];
+        ls.pre[tid] = wbase + inc - nr;
+        uint32_t items = 0;
+        for (uint32_t w = 0; w < kTileThreads / 64u; w++) items += ls.wsum[w];
+        const uint32_t staged = min(kTileStage, n - c0);
+        __syncthreads();
+        for (uint32_t it = tid; it < items; it += kTileThreads) {
+            uint32_t lo = 0, hi = staged - 1u;           // last k with pre[k] <= it
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1u) >> 1;
+                if (ls.pre[mid] <= it) lo = mid; else hi = mid - 1u;
+            }
+            const uint32_t k = lo;
+            const uint32_t lr = ls.r0[k] + (it - ls.pre[k]);
+            const uint32_t y = row_of(lr);
+            const uint32_t xmin = ls.xmin[k];
+            const uint32_t x0 = max(xmin, lx0), x1 = min(ls.xmax[k], lx1);
+            float w[3], d[3], r[3];
+#pragma unroll
+            for (uint32_t c = 0; c < 3; c++) {
+                d[c] = ls.dx[c][k];
+                r[c] = ls.rz[c][k];
+                w[c] = short_walk(short_walk(ls.ws[c][k], ls.dy[c][k], y - ls.ymin[k]), d[c], x0 - xmin);
+            }
+            const unsigned long long low = 0xFFFFFFFFull - ls.slot[k];
+            unsigned long long *krow = ls.key + (lr - tr0) * kKeyStride - lx0;
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 4)
+            if (x1 == 0xFFFFFFFFu)                      // ablation: no pixel loop
+#endif
+            for (uint32_t x = x0; x <= x1; x++) {
+                if (w[0] >= 0 && w[1] >= 0 && w[2] >= 0) {                        // :362
+                    const float ooz = (r[0] * w[0] + r[1] * w[1]) + r[2] * w[2];  // :363
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 2)
+                    if (ooz == 1234.5f) krow[x] = low;          // ablation: no LDS atomic
+#else
+                    if (ooz > 0.0f) atomicMax(krow + x, ((unsigned long long)f2u(ooz) << 32) | low);
+#endif
+                }
+                w[0] = w[0] + d[0]; w[1] = w[1] + d[1]; w[2] = w[2] + d[2];    // :374
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {
+        const uint32_t rr = i / kTileW, cc = i % kTileW;
+        const uint32_t lr = tr0 + rr, x = lx0 + cc;
+        if (lr <= tr1 && x <= lx1) keys[(size_t)lr * W + x] = ls.key[rr * kKeyStride + cc];
+    }
+}
+
+// One thread per pixel: the winner of each pixel (key), re-walked exactly from its raster record
+// and shaded with constants recomputed from the scene (slot_setup); background where no fragment.
+__global__ void __launch_bounds__(256) k_tile_resolve(
+    const unsigned long long *__restrict__ keys, const RasterRec *__restrict__ recs, const float4 *__restrict__ vtx,
+    const float4 *__restrict__ nrm, const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
+    const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
+    float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
+    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local) {
+    const uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
+    const uint32_t lr = blockIdx.y * 4u + (threadIdx.x >> 6);
+    if (x >= W || lr >= rows_local) return;
+    const size_t idx = (size_t)lr * W + x;
+    const unsigned long long k = keys[idx];
+    uint32_t v = kBackground;
+    if (k) {
+        const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
+        const float ooz = u2f((uint32_t)(k >> 32));
+        const float4 *q = reinterpret_cast<const float4 *>(recs + s);
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
+        const uint32_t y = ((lr / band) * nparts + part) * band + lr % band;
+        const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
+        const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
+        const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
+        TriSetup ts;
+        slot_setup(s, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, sw, sh, ts);
+        v = shade(&ts, w0, w1, w2, ooz, tex, ntex);
+    }
+    out[idx] = v;
+}
+
 // ------------------------------------------------------------------ self-test kernel
 // Batch evaluation of exact_walk / chunk_linear on the device, for tests/test_exact_walk.py.
 __global__ void __launch_bounds__(256) k_walk_test(const float *s, const float *d, const uint32_t *n, float *out,
@@ -924,6 +1291,52 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_fragment<kSegChunks>, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab,
                        tex, ntex, out, W, H, band, nparts, part, segs, rows_local, (const Entry *)bins, counts);
+}
+
+uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
+uint32_t tile_count(uint32_t W, uint32_t rows_local) { return tile_grid_x(W) * ((rows_local + kTileH - 1) / kTileH); }
+size_t raster_rec_bytes() { return sizeof(RasterRec); }
+
+void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
+                       float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                       void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
+                       uint32_t *offs, uint32_t *cursor, uint32_t *total, hipStream_t st) {
+    const uint32_t nt = tile_count(W, rows_local);
+    (void)hipMemsetAsync(counts, 0, sizeof(uint32_t) * nt, st);
+    (void)hipMemsetAsync(app_count, 0, sizeof(uint32_t), st);
+    if (ntri)
+        hipLaunchKernelGGL(k_tile_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor, sw, sh,
+                           band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count, counts);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, counts, nt, offs, cursor, total);
+}
+
+void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
+                      uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
+                      hipStream_t st) {
+    const uint64_t n = (uint64_t)ntri + napp;
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_tile_fill, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, boxes, ntri,
+                       (const RasterRec *)recs, app_list, napp, band, nparts, part, tile_grid_x(W), cursor, list);
+}
+
+void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                        uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
+                        unsigned long long *keys, hipStream_t st) {
+    const uint32_t nt = tile_count(W, rows_local);
+    if (nt == 0) return;
+    hipLaunchKernelGGL(k_tile_raster, dim3(nt), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band, nparts,
+                       part, rows_local, tile_grid_x(W), offs, counts, list, keys);
+}
+
+void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
+                         const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
+                         uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
+                         uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                         uint32_t rows_local, hipStream_t st) {
+    if (W == 0 || rows_local == 0) return;
+    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64, (rows_local + 3) / 4), dim3(256), 0, st, keys,
+                       (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex, ntex,
+                       out, W, band, nparts, part, rows_local);
 }
 
 }  // namespace s3r

@@ -63,6 +63,18 @@ struct Lib {
     void *bins[2] = {nullptr, nullptr};        // per-workgroup triangle lists (k_bin)
     uint32_t *bin_counts[2] = {nullptr, nullptr};
     uint64_t bins_cap = 0;
+    // tile path (many triangles): per-tile counts, offsets, scatter cursors, slot lists
+    uint32_t *tile_counts[2] = {nullptr, nullptr}, *tile_offs[2] = {nullptr, nullptr};
+    uint32_t *tile_cursor[2] = {nullptr, nullptr}, *tile_total[2] = {nullptr, nullptr};
+    uint32_t *tile_list[2] = {nullptr, nullptr};
+    void *recs[2] = {nullptr, nullptr};        // 2T raster records (positions-only setup)
+    uint32_t *boxes[2] = {nullptr, nullptr};   // T packed bboxes
+    uint32_t *app_list[2] = {nullptr, nullptr}, *app_count[2] = {nullptr, nullptr};
+    uint64_t tiles_cap = 0, tile_list_cap[2] = {0, 0};
+    unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
+    size_t keys_cap = 0;
+    uint32_t *tile_total_host = nullptr;       // pinned: (total, appended) per buffer set
+    int raster_path = 0;                       // 0 auto, 1 rows (k_bin + k_fragment), 2 tiles
     hipEvent_t geo_done[2] = {nullptr, nullptr}, frag_done[2] = {nullptr, nullptr};
     uint32_t parity = 0;
     uint32_t *frame = nullptr;
@@ -245,9 +257,14 @@ void release_all() {
         (void)hipDeviceSynchronize();
         unregister_all();
         void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.tris[0], g.tris[1], g.frame,
-                        g.rowtab[0], g.rowtab[1], g.bins[0], g.bins[1], g.bin_counts[0], g.bin_counts[1]};
+                        g.rowtab[0], g.rowtab[1], g.bins[0], g.bins[1], g.bin_counts[0], g.bin_counts[1],
+                        g.tile_counts[0], g.tile_counts[1], g.tile_offs[0], g.tile_offs[1], g.tile_cursor[0],
+                        g.tile_cursor[1], g.tile_list[0], g.tile_list[1],  // tile_total aliases app_count
+                        g.recs[0], g.recs[1], g.boxes[0], g.boxes[1], g.app_list[0], g.app_list[1],
+                        g.app_count[0], g.app_count[1], g.keys};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
+        if (g.tile_total_host) (void)hipHostFree(g.tile_total_host);
         for (int p = 0; p < 2; p++) {
             if (g.geo_done[p]) (void)hipEventDestroy(g.geo_done[p]);
             if (g.frag_done[p]) (void)hipEventDestroy(g.frag_done[p]);
@@ -259,11 +276,12 @@ void release_all() {
         if (g.stream) (void)hipStreamDestroy(g.stream);
     }
     const std::string path = g.data_path;
-    const int dev = g.device;
+    const int dev = g.device, rp = g.raster_path;
     g.~Lib();
     new (&g) Lib();
     g.data_path = path;
     g.device = dev;
+    g.raster_path = rp;
 }
 
 // render.cpp:266-280: first-call init, camera, resize.
@@ -294,9 +312,92 @@ TimingSlot *timing_slot() {
     return &g.tslots[g.tcount++];
 }
 
+// Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
+// the order-independent tile path takes over (the icosahedron stress scene).
+constexpr uint64_t kRowPathMaxSlots = 8192;
+
+bool use_tile_path() {
+    if (g.raster_path == 1) return false;
+    if (g.raster_path == 2) return true;
+    return 2ull * g.ntri > kRowPathMaxSlots;
+}
+
+void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                  uint32_t *out, hipStream_t st, TimingSlot *ts) {
+    if (W > 65535 || H > 65535) {                       // packed 16-bit bboxes
+        fprintf(stderr, "s3r: tile path supports frames up to 65535 x 65535\n");
+        exit(1);
+    }
+    const float sw = (float)W, sh = (float)H;
+    const uint64_t nt = tile_count(W, rows_local);
+    if (g.tiles_cap < nt) {
+        HIPCHECK(hipDeviceSynchronize());
+        for (int p = 0; p < 2; p++) {
+            for (uint32_t **q : {&g.tile_counts[p], &g.tile_offs[p], &g.tile_cursor[p]}) {
+                if (*q) HIPCHECK(hipFree(*q));
+                *q = dalloc<uint32_t>(nt);
+            }
+        }
+        g.tiles_cap = nt;
+    }
+    const size_t npx = (size_t)W * rows_local;
+    if (g.keys_cap < npx) {                    // per-pixel winners (fragment stage, caller's stream)
+        HIPCHECK(hipDeviceSynchronize());
+        if (g.keys) HIPCHECK(hipFree(g.keys));
+        g.keys = dalloc<unsigned long long>(npx);
+        g.keys_cap = npx;
+    }
+    if (!g.recs[0]) {
+        for (int p = 0; p < 2; p++) {
+            g.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
+            g.boxes[p] = dalloc<uint32_t>((size_t)2 * g.ntri);
+            g.app_list[p] = dalloc<uint32_t>(g.ntri);
+            g.app_count[p] = dalloc<uint32_t>(2);          // [0] appended count, [1] tile-pair total
+            g.tile_total[p] = g.app_count[p] + 1;
+        }
+        HIPCHECK(hipHostMalloc((void **)&g.tile_total_host, 4 * sizeof(uint32_t)));
+    }
+    const uint32_t p = g.parity;
+    g.parity ^= 1u;
+    HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
+    if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
+    launch_tile_setup(g.vtx, g.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, g.recs[p],
+                      g.boxes[p], g.app_list[p], g.app_count[p], g.tile_counts[p], g.tile_offs[p], g.tile_cursor[p],
+                      g.tile_total[p], g.geo);
+    // the list size is data-dependent: read it back (the tile path's one host sync per frame)
+    uint32_t *host = g.tile_total_host + 2 * p;
+    HIPCHECK(hipMemcpyAsync(host, g.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, g.geo));
+    HIPCHECK(hipStreamSynchronize(g.geo));
+    const uint32_t napp = host[0];
+    const uint64_t total = host[1];
+    if (g.tile_list_cap[p] < total) {
+        HIPCHECK(hipDeviceSynchronize());
+        if (g.tile_list[p]) HIPCHECK(hipFree(g.tile_list[p]));
+        const uint64_t cap = total + total / 4 + 1024;
+        g.tile_list[p] = dalloc<uint32_t>(cap);
+        g.tile_list_cap[p] = cap;
+    }
+    launch_tile_fill(g.boxes[p], g.ntri, g.recs[p], g.app_list[p], napp, W, band, nparts, part, g.tile_cursor[p],
+                     g.tile_list[p], g.geo);
+    HIPCHECK(hipEventRecord(g.geo_done[p], g.geo));
+    HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
+    if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
+    launch_tile_raster(g.recs[p], W, band, nparts, part, rows_local, g.tile_offs[p], g.tile_counts[p], g.tile_list[p],
+                       g.keys, st);
+    launch_tile_resolve(g.keys, g.recs[p], g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh,
+                        g.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
+    if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
+    HIPCHECK(hipEventRecord(g.frag_done[p], st));
+    HIPCHECK(hipGetLastError());
+}
+
 void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st) {
     TimingSlot *ts = timing_slot();
+    if (use_tile_path()) {
+        render_tiles(W, H, band, nparts, part, rows_local, out, st, ts);
+        return;
+    }
     const float sw = (float)W, sh = (float)H;
     const size_t need = (size_t)2 * g.ntri * H * (fragment_segments(W) + 1) * 4;
     if (g.rowtab_cap < need) {
@@ -381,6 +482,14 @@ __attribute__((visibility("default"))) int s3r_configure(const char *data_path, 
 }
 
 __attribute__((visibility("default"))) void s3r_shutdown(void) { release_all(); }
+
+__attribute__((visibility("default"))) int s3r_set_raster_path(int mode) {
+    if (mode < 0 || mode > 2) return -1;
+    g.raster_path = mode;
+    return 0;
+}
+
+__attribute__((visibility("default"))) int s3r_raster_path(void) { return use_tile_path() ? 2 : 1; }
 
 __attribute__((visibility("default"))) uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows,
                                                                    uint32_t n_parts, uint32_t part) {

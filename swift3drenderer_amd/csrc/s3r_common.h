@@ -112,6 +112,16 @@ S3R_HD float exact_walk(float s, float d, uint32_t n, uint32_t *iters = nullptr)
     return s;
 }
 
+// exact_walk for walks that are usually short (small triangles): up to kSeqWalk steps are the
+// reference's own sequential adds (one add per step; exact_walk would single-step them anyway near
+// zero and across binades, at ~40 instructions a step), longer walks jump.
+constexpr uint32_t kSeqWalk = 48;
+S3R_HD float short_walk(float s, float d, uint32_t n) {
+    if (n > kSeqWalk) return exact_walk(s, d, n);
+    for (uint32_t i = 0; i < n; i++) s = s + d;
+    return s;
+}
+
 // Length of the linear run starting at c: the largest j such that S(c, d, k) == c + k*delta for
 // every k <= j (0: not even one regular step; +inf: the walk has stagnated, delta == 0).
 S3R_HD float linear_run(float c, float d, float *delta) {

@@ -29,6 +29,27 @@ uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
 
+// Tile path (order-independent fragment stage for many triangles): tiles of 16 local rows x 64 px.
+// recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts/offs/cursor: tile_count().
+uint32_t tile_count(uint32_t W, uint32_t rows_local);
+size_t raster_rec_bytes();
+void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
+                       float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                       void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
+                       uint32_t *offs, uint32_t *cursor, uint32_t *total, hipStream_t st);
+void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
+                      uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
+                      hipStream_t st);
+// keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
+void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                        uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
+                        unsigned long long *keys, hipStream_t st);
+void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
+                         const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
+                         uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
+                         uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                         uint32_t rows_local, hipStream_t st);
+
 void stats_read(unsigned long long out[16], bool reset);
 
 void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,

@@ -16,8 +16,8 @@ from .abi import Input, pixel_data_for
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 
-EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_render_bands', 's3r_band_rows_local',
-           's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
+EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_set_raster_path', 's3r_raster_path',
+           's3r_render_bands', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
 
 _lib = None
 
@@ -35,6 +35,10 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.s3r_configure.restype = ctypes.c_int
     lib.s3r_shutdown.argtypes = []
+    lib.s3r_set_raster_path.argtypes = [ctypes.c_int]
+    lib.s3r_set_raster_path.restype = ctypes.c_int
+    lib.s3r_raster_path.argtypes = []
+    lib.s3r_raster_path.restype = ctypes.c_int
     lib.s3r_render_bands.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     lib.s3r_render_bands.restype = ctypes.c_int64
@@ -87,6 +91,15 @@ class Renderer:
         if r < 0:
             raise ValueError('s3r_render_bands: bad arguments')
         return int(r)
+
+    def set_raster_path(self, mode: str | int):
+        """'auto' | 'rows' | 'tiles' (or 0/1/2): the fragment-stage strategy, include/render.h."""
+        m = {'auto': 0, 'rows': 1, 'tiles': 2}.get(mode, mode)
+        if self.lib.s3r_set_raster_path(int(m)) != 0:
+            raise ValueError(f'unknown raster path {mode!r}')
+
+    def raster_path(self) -> str:
+        return {1: 'rows', 2: 'tiles'}[self.lib.s3r_raster_path()]
 
     def timing(self, enable: bool):
         self.lib.s3r_timing(1 if enable else 0)

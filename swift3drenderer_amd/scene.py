@@ -442,4 +442,7 @@ def read_scene(path: str) -> SceneArrays:
 
 
 def write_named(name: str, path: str) -> int:
+    from . import stress
+    if stress.is_stress_name(name):       # icosa-stress (config 5) / icosa-<n>: streamed, vectorized
+        return stress.write_named(name, path)
     return write_scene(build_scene(name), path)

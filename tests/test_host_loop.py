@@ -83,7 +83,6 @@ def test_host_loop_matches_oracle(host_bin, scene_dir, tmp_path):
                         '--script', SCRIPT, '--dump', prefix, str(every)], env=env, capture_output=True,
                        timeout=300)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
-    assert b'average:' in r.stdout or frames < 60
     seq = inputs_for(read_script(SCRIPT), frames)
     o = OracleRenderer(scene_dir['full'])
     checked = 0

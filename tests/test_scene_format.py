@@ -107,3 +107,41 @@ def test_splitmix_known_answer():
     # SplitMix64 reference values for seed 1234567 (Vigna's splitmix64.c)
     r = scene.SplitMix64(1234567)
     assert [r.next_u64() for _ in range(3)] == [6457827717110365317, 3203168211198807973, 9817491932198370423]
+
+
+def test_stress_scene_layout_and_determinism(tmp_path):
+    """The icosahedron stress generator (config 5): data.bin layout, size formula, cross-check of
+    one icosahedron against the scalar addIcosahedron restatement, and a pinned digest."""
+    from swift3drenderer_amd import stress
+    p = str(tmp_path / 'i500.bin')
+    n = stress.write_stress(p, 500, seed=1)
+    assert n == stress.expected_size(500) == len(open(p, 'rb').read())
+    s = scene.read_scene(p)
+    assert s.vertices.shape == (6000, 4) and np.all(s.vertices[:, 3] == 1)
+    assert np.array_equal(s.attribute_indices, np.arange(30000))
+    assert s.vertex_indices[:60].tolist() == [v for f in scene.ICOSA_FACES for v in f]
+    assert s.vertex_indices.max() == 5999 and s.texels.size == 0
+    assert np.all(s.attributes[:, 32] == 0)                       # colour tag
+    z = s.vertices[:, 2]
+    assert z.max() < -4.9 and z.min() > -60.5
+    with open(p, 'rb') as f:
+        assert hashlib.sha256(f.read()).hexdigest() == \
+            '1edf44cfbed40516b3ae72494776ec0c455f489db36f58552ba8d007048b7ef6'
+    assert stress.is_stress_name('icosa-stress') and stress.count_of('icosa-stress') == 1_000_000
+    assert stress.count_of('icosa-2000') == 2000 and not stress.is_stress_name('full')
+
+
+def test_stress_matches_scalar_icosahedron():
+    from swift3drenderer_amd import stress
+    ids = np.arange(7, 8, dtype=np.uint64)
+    x, y, z = stress._frames(1, ids)
+    v, nrm = stress._chunk(1, 7, 8)
+    uv = scene.icosa_unit_vertices(*[tuple(np.float32(c) for c in a[0]) for a in (x, y, z)])
+    depth = stress._uniform(1, 4, ids, *stress.DEPTH)
+    cx = stress._uniform(1, 5, ids, -1.05, 1.05) * stress.HALF_X * depth
+    cy = stress._uniform(1, 6, ids, -1.05, 1.05) * stress.HALF_Y * depth
+    r = depth * stress._uniform(1, 7, ids, *stress.RADIUS_PER_DEPTH)
+    vv = [scene.add(scene.smul(r[0], q), (cx[0], cy[0], -depth[0])) for q in uv]
+    assert np.array_equal(np.array(vv, dtype=np.float32), v[0])
+    nn = [scene.tri_normal(vv, a, b, c) for a, b, c in scene.ICOSA_FACES]
+    assert np.array_equal(np.array(nn, dtype=np.float32), nrm[0])

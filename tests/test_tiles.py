@@ -1,0 +1,115 @@
+"""The tile path (order-independent fragment stage, include/render.h s3r_set_raster_path): the same
+frames as the CPU oracle, bit for bit -- on the packaged scenes (tile path forced) and on the
+icosahedron stress scenes (BASELINE config 5; the path the library picks for them itself)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.oracle import render_pose as oracle_render_pose
+from swift3drenderer_amd import poses, stress
+from swift3drenderer_amd.renderer import render_pose
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def tiles(gpu_renderer):
+    gpu_renderer.set_raster_path('tiles')
+    yield gpu_renderer
+    gpu_renderer.set_raster_path('auto')
+
+
+@pytest.fixture(scope='module')
+def icosa_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp('icosa')
+    out = {}
+    for n in (2000, 100000):
+        p = str(d / f'icosa-{n}.bin')
+        stress.write_stress(p, n, seed=1)
+        out[n] = p
+    return out
+
+
+def diff(a, b):
+    from test_gpu_parity import diff_report
+    return diff_report(a, b)
+
+
+FORCED = [
+    ('full', 'P_id', 640, 480),
+    ('full', 'P_over', 640, 480),
+    ('full', 'P_clip', 640, 480),
+    ('full', 'P_floor', 640, 480),
+    ('flat', 'P_over', 1920, 1080),
+    ('tetra', 'P_tetra', 640, 480),
+    ('regular', 'P_over', 1280, 720),
+    ('full', 'P_over', 1000, 333),
+    ('full', 'P_id', 17, 5),
+]
+
+
+@pytest.mark.parametrize('scene_name,pose,w,h', FORCED)
+def test_tiles_match_oracle_packaged(tiles, scene_dir, scene_name, pose, w, h):
+    path = scene_dir[scene_name]
+    script = poses.script(pose)
+    want = oracle_render_pose(path, script, w, h, extra_frames=1)
+    got = render_pose(tiles, path, script, w, h, extra_frames=1)
+    assert tiles.raster_path() == 'tiles'
+    assert np.array_equal(got, want), diff(got, want)
+
+
+@pytest.mark.parametrize('pose,w,h', [('P_id', 1920, 1080), ('P_id', 3840, 2160), ('P_strafe', 1280, 720)])
+def test_stress_small_matches_oracle(gpu_renderer, icosa_dir, pose, w, h):
+    path = icosa_dir[2000]
+    script = poses.script(pose)
+    want = oracle_render_pose(path, script, w, h, extra_frames=1)
+    got = render_pose(gpu_renderer, path, script, w, h, extra_frames=1)
+    assert gpu_renderer.raster_path() == 'tiles'      # 40 000 slots: chosen automatically
+    assert np.array_equal(got, want), diff(got, want)
+
+
+def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir):
+    """100 000 icosahedra (2 M triangles) at 3840x2160 -- a tenth of config 5, oracle-checkable."""
+    path = icosa_dir[100000]
+    script = poses.script('P_id')
+    want = oracle_render_pose(path, script, 3840, 2160)
+    got = render_pose(gpu_renderer, path, script, 3840, 2160)
+    assert (want != 0x1E1E1E).mean() > 0.9            # the view is filled
+    assert np.array_equal(got, want), diff(got, want)
+
+
+@pytest.mark.parametrize('band,nparts', [(16, 2), (16, 3), (5, 2), (7, 4)])
+def test_tile_bands_reassemble(gpu_renderer, icosa_dir, band, nparts):
+    """Row bands rendered separately on the tile path == the whole frame (multi-GPU exactness)."""
+    import torch
+    from swift3drenderer_amd.multi import assemble
+    W, H = 1280, 720
+    path = icosa_dir[2000]
+    r = gpu_renderer
+    r.configure(path)
+    inp = (0, 0, 0, 0, 0, 0)
+    full = r.update_and_render(W, H, inp)
+    parts = []
+    for part in range(nparts):
+        rows = r.lib.s3r_band_rows_local(H, band, nparts, part)
+        buf = torch.empty((max(rows, 1), W), dtype=torch.int32, device='cuda')
+        r.render_bands(inp, W, H, band, nparts, part, buf.data_ptr(), 0)
+        torch.cuda.synchronize()
+        parts.append(buf[:rows].cpu().numpy().view(np.uint32))
+    got = assemble(parts, H, band)
+    assert np.array_equal(got, full), diff(got, full)
+
+
+def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
+    """Row path and tile path give the same 4K frame (both are exact)."""
+    path = scene_dir['full']
+    script = poses.script('P_over')
+    gpu_renderer.set_raster_path('rows')
+    a = render_pose(gpu_renderer, path, script, 3840, 2160)
+    gpu_renderer.set_raster_path('tiles')
+    try:
+        b = render_pose(gpu_renderer, path, script, 3840, 2160)
+    finally:
+        gpu_renderer.set_raster_path('auto')
+    assert np.array_equal(a, b), diff(a, b)

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""Build tuning variants here (tools/variants.py build) and time them on the GPU box
-(tools/variants.py run): fragment-kernel ms per variant, interleaved rounds in separate processes."""
-import json
+"""Build tuning / ablation variants here (tools/variants.py build) and time them on the GPU box
+(tools/variants.py run): per-kernel average us from rocprofv3 --kernel-trace --stats per variant.
+Env: S3R_VARIANT_BENCH = extra bench.py args (default: the stress scene)."""
+import csv
+import glob
 import os
+import shlex
 import subprocess
 import sys
 
@@ -10,10 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
-    'calls': {'S3R_INLINE': 0},
-    'inline': {'S3R_INLINE': 1},
-    'inline_skel': {'S3R_INLINE': 1, 'S3R_ABLATE': 189},
-    'calls_skel': {'S3R_INLINE': 0, 'S3R_ABLATE': 189},
+    'base': {},
+    'tab1': {'S3R_TABLATE': 1},     # setup without tile counting
+    'tab2': {'S3R_TABLATE': 2},     # raster without the LDS atomic
+    'tab4': {'S3R_TABLATE': 4},     # raster without the pixel loop
 }
 
 
@@ -23,19 +26,24 @@ def build():
         print(build_variant(tag, d))
 
 
-def run(poses=('P_over', 'P_id')):
-    res = {}
-    for rnd in range(2):
-        for tag in VARIANTS:
-            for pose in poses:
-                env = dict(os.environ, S3R_LIB=os.path.join(ROOT, 'build', f'librender_{tag}.so'))
-                out = subprocess.run([sys.executable, 'bench.py', '--pose', pose, '--steps', '100', '--warmup', '10',
-                                      '--no-cpu-baseline', '--no-e2e'], env=env, capture_output=True, text=True,
-                                     timeout=120, cwd=ROOT)
-                d = json.loads(out.stdout.strip().splitlines()[-1])
-                res.setdefault((tag, pose), []).append((d['fragment_kernel_ms'], d['value']))
-    for (tag, pose), v in sorted(res.items()):
-        print(f'{tag:14s} {pose:8s} frag_ms {min(a for a, _ in v):.4f}  fps {max(b for _, b in v):9.1f}  rounds {v}')
+def run():
+    extra = shlex.split(os.environ.get('S3R_VARIANT_BENCH', '--scene icosa-stress --pose P_id'))
+    out_root = os.path.join(ROOT, 'gpurun_out', 'variants')
+    for tag in VARIANTS:
+        env = dict(os.environ, S3R_LIB=os.path.join(ROOT, 'build', f'librender_{tag}.so'), TMPDIR='/tmp')
+        d = os.path.join(out_root, tag)
+        cmd = ['rocprofv3', '--kernel-trace', '--stats', '-d', d, '-o', 'run', '--output-format', 'csv', '--',
+               sys.executable, 'bench.py', '--steps', '10', '--warmup', '2', '--no-cpu-baseline', '--no-e2e'] + extra
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+        line = [l for l in r.stdout.splitlines() if l.startswith('{')]
+        fps = line[-1].split('"value": ')[1].split(',')[0] if line else '?'
+        stats = glob.glob(os.path.join(d, '**', 'run_kernel_stats.csv'), recursive=True)
+        parts = []
+        if stats:
+            for row in csv.DictReader(open(stats[0])):
+                if row['Name'].startswith('s3r::'):
+                    parts.append(f"{row['Name'][5:].split('(')[0]} {float(row['AverageNs']) / 1e3:.1f}")
+        print(f'{tag:8s} fps {fps:>10s}  ' + '  '.join(parts), flush=True)
 
 
 if __name__ == '__main__':
