@@ -871,7 +871,11 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
 //                  Each pixel's winner is then re-walked exactly and shaded; its shading constants
 //                  (normals, colours / uvs: the attribute stream) are recomputed from the scene by the
 //                  same setup code, so attributes are read only for visible triangles.
-constexpr uint32_t kTileW = 64, kTileH = 16, kTileThreads = 256, kTileStage = 256;
+#ifndef S3R_TSTAGE
+#define S3R_TSTAGE 128
+#endif
+constexpr uint32_t kTileW = 64, kTileH = 16, kTileThreads = 256, kTileStage = S3R_TSTAGE;
+static_assert(kTileStage <= kTileThreads, "one staged triangle per thread at most");
 constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of one column hit different banks
 constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
 
@@ -1055,6 +1059,7 @@ struct TileShared {
     float ws[3][kTileStage], dx[3][kTileStage], dy[3][kTileStage], rz[3][kTileStage];
     uint32_t slot[kTileStage], xmin[kTileStage], xmax[kTileStage], ymin[kTileStage], r0[kTileStage];
     uint32_t pre[kTileStage + 1];
+    uint16_t item[kTileStage * kTileH];            // item -> staged triangle
     uint32_t wsum[kTileThreads / 64];
 };
 
@@ -1104,7 +1109,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         __syncthreads();                                 // previous stage fully consumed
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
-        if (j < n) {
+        if (tid < kTileStage && j < n) {
             const uint32_t s = list[base + j];
             const float4 *q = reinterpret_cast<const float4 *>(recs + s);
             const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
@@ -1130,18 +1135,14 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         __syncthreads();
         uint32_t wbase = 0;
         for (uint32_t w = 0; w < wave; w++) wbase += ls.wsum[w];
-        ls.pre[tid] = wbase + inc - nr;
+        if (tid < kTileStage) ls.pre[tid] = wbase + inc - nr;
         uint32_t items = 0;
         for (uint32_t w = 0; w < kTileThreads / 64u; w++) items += ls.wsum[w];
-        const uint32_t staged = min(kTileStage, n - c0);
+        if (tid < kTileStage)
+            for (uint32_t i = 0; i < nr; i++) ls.item[ls.pre[tid] + i] = (uint16_t)tid;
         __syncthreads();
         for (uint32_t it = tid; it < items; it += kTileThreads) {
-            uint32_t lo = 0, hi = staged - 1u;           // last k with pre[k] <= it
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1u) >> 1;
-                if (ls.pre[mid] <= it) lo = mid; else hi = mid - 1u;
-            }
-            const uint32_t k = lo;
+            const uint32_t k = ls.item[it];
             const uint32_t lr = ls.r0[k] + (it - ls.pre[k]);
             const uint32_t y = row_of(lr);
             const uint32_t xmin = ls.xmin[k];
@@ -1163,6 +1164,9 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
                     const float ooz = (r[0] * w[0] + r[1] * w[1]) + r[2] * w[2];  // :363
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 2)
                     if (ooz == 1234.5f) krow[x] = low;          // ablation: no LDS atomic
+#elif defined(S3R_TPRECHECK) && S3R_TPRECHECK
+                    const unsigned long long kv = ((unsigned long long)f2u(ooz) << 32) | low;
+                    if (ooz > 0.0f && kv > krow[x]) atomicMax(krow + x, kv);   // plain read first
 #else
                     if (ooz > 0.0f) atomicMax(krow + x, ((unsigned long long)f2u(ooz) << 32) | low);
 #endif

@@ -14,6 +14,8 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     'base': {},
+    'pre': {'S3R_TPRECHECK': 1},    # plain LDS read before the atomic
+    'st256': {'S3R_TSTAGE': 256},
     'tab1': {'S3R_TABLATE': 1},     # setup without tile counting
     'tab2': {'S3R_TABLATE': 2},     # raster without the LDS atomic
     'tab4': {'S3R_TABLATE': 4},     # raster without the pixel loop
