@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 METRIC = 'frames/sec + Mpixels/s at 3840x2160, data.bin scene; 1/2/4/8-GPU scaling'
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md, HBM3E peak (spec)
 TRI_SETUP_BYTES = 240    # sizeof(TriSetup)
+RASTER_REC_BYTES = 64    # sizeof(RasterRec), tile path
 
 
 def parse():
@@ -71,7 +72,7 @@ def cpu_baseline(data_path, script, hold, w, h, budget_s):
         r.update_and_render(w, h, hold, out)
         frames += 1
         el = time.perf_counter() - t0
-        if (el >= budget_s and frames >= 3) or frames >= 2000:
+        if (el >= budget_s and frames >= 3) or el >= 3 * budget_s or frames >= 2000:
             break
     return frames / el, frames, el
 
@@ -169,11 +170,18 @@ def main():
         el = float(t.item())
 
     fps = a.steps / el
-    counts = r.scene_counts()      # V, I, A, texels, slots
-    nv, ni, na, ntex, nslots = counts[:5]
-    # algorithmic bytes of the fragment kernel per launch: this rank's framebuffer rows + the
-    # ripmap texels it may sample + the triangle setup records it reads
-    frag_bytes = 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
+    counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
+    nv, ni, na, ntex, nslots, pairs, path = counts[:7]
+    if path == 2:
+        # tile path, fragment stage = k_tile_raster + k_tile_resolve: framebuffer rows, the per-pixel
+        # (1/z, slot) keys written and read back, and per (slot, tile) pair its list entry + 64-B record
+        kernel = 'k_tile_raster+k_tile_resolve'
+        frag_bytes = 4 * W * rows + 16 * W * rows + (4 + RASTER_REC_BYTES) * pairs
+    else:
+        # row path, k_fragment: this rank's framebuffer rows + the ripmap texels it may sample + the
+        # triangle setup records it reads
+        kernel = 'k_fragment'
+        frag_bytes = 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
     frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
     achieved = frag_bytes / frag_avg_s / 1e9
     workload = f'{a.scene}/{a.pose}/{W}x{H}/N{N}'
@@ -215,6 +223,7 @@ def main():
             'data': 'synthetic: deterministic data.bin-format scene (SplitMix64 geometry, procedural ripmaps)',
             'config': {'workload': f'updateAndRender frame, scene {a.scene} ({nslots // 2} triangles, '
                                    f'{ntex >> 18} ripmap textures), pose {a.pose}, {W}x{H}',
+                       'fragment_path': {1: 'rows', 2: 'tiles'}.get(path, '?'),
                        'scene': a.scene, 'pose': a.pose, 'width': W, 'height': H,
                        'band_rows': B if N > 1 else H, 'parallelism': f'rows{N}' + ('+gather' if N > 1 else '')},
             'mpixels_per_s': round(fps * W * H / 1e6, 2),
@@ -223,7 +232,7 @@ def main():
             'e2e_fps_with_d2h': round(e2e, 3) if e2e else None,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
-                         'kernel': 'k_fragment', 'algorithmic_bytes_per_launch': frag_bytes},
+                         'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes},
             'cpu_baseline': cpu,
         }
         print(json.dumps(result), flush=True)

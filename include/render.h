@@ -83,7 +83,8 @@ uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_par
 void s3r_timing(int enable);
 void s3r_timing_collect(double out[3]);
 
-/* Scene counts after init: out = {vertices, indices, attributes, texels, triangle slots, 0, 0, 0}. */
+/* Scene counts after init: out = {vertices, indices, attributes, texels, triangle slots,
+ * (slot, tile) pairs binned in the last frame (tile path), the last frame's path (1 rows, 2 tiles), 0}. */
 void s3r_scene_counts(uint64_t out[8]);
 
 /* Copy the current camera matrix (3 rows x 4) and raster factor. */

@@ -899,6 +899,7 @@ __device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint
 // row order is frame row order, so the owned rows of any frame-row interval are one local range).
 __device__ __forceinline__ bool local_row_range(uint32_t ymin, uint32_t ymax, uint32_t band, uint32_t nparts,
                                                 uint32_t part, uint32_t &lo, uint32_t &hi) {
+    if (nparts == 1u) { lo = ymin; hi = ymax; return ymin <= ymax; }
     const uint32_t g0 = ymin / band, g1 = ymax / band;
     uint32_t fg = g0, fy = ymin;
     if (g0 % nparts != part) { fg = g0 + (part + nparts - g0 % nparts) % nparts; fy = fg * band; }
@@ -1102,17 +1103,28 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const uint32_t tile = blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t lx0 = tx * kTileW, lx1 = min(W, lx0 + kTileW) - 1u;
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
-    auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
+    auto row_of = [&](uint32_t lr) { return nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band; };
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
     const uint32_t n = counts[tile], base = offs[tile];
+    // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
+    // while stage c0's items run
+    uint32_t s_nx = 0;
+    float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n, q3n = q0n;
+    auto fetch = [&](uint32_t c) {
+        if (tid < kTileStage && c + tid < n) {
+            s_nx = list[base + c + tid];
+            const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
+            q0n = q[0]; q1n = q[1]; q2n = q[2]; q3n = q[3];
+        }
+    };
+    fetch(0);
     for (uint32_t c0 = 0; c0 < n; c0 += kTileStage) {
         __syncthreads();                                 // previous stage fully consumed
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
         if (tid < kTileStage && j < n) {
-            const uint32_t s = list[base + j];
-            const float4 *q = reinterpret_cast<const float4 *>(recs + s);
-            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            const uint32_t s = s_nx;
+            const float4 q0 = q0n, q1 = q1n, q2 = q2n, q3 = q3n;
             const uint32_t bx = f2u(q0.x), by = f2u(q0.y);
             uint32_t lo = 1u, hi = 0u;
             local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi);
@@ -1125,6 +1137,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             ls.dy[0][tid] = q2.z; ls.dy[1][tid] = q2.w; ls.dy[2][tid] = q3.x;
             ls.rz[0][tid] = q3.y; ls.rz[1][tid] = q3.z; ls.rz[2][tid] = q3.w;
         }
+        fetch(c0 + kTileStage);
         // exclusive scan of the row counts over the stage (wave shuffles + wave totals)
         uint32_t inc = nr;
         for (uint32_t o = 1; o < 64u; o <<= 1) {
@@ -1138,9 +1151,45 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         if (tid < kTileStage) ls.pre[tid] = wbase + inc - nr;
         uint32_t items = 0;
         for (uint32_t w = 0; w < kTileThreads / 64u; w++) items += ls.wsum[w];
+#if !(defined(S3R_TITEM) && S3R_TITEM)
         if (tid < kTileStage)
             for (uint32_t i = 0; i < nr; i++) ls.item[ls.pre[tid] + i] = (uint16_t)tid;
         __syncthreads();
+#endif
+#if defined(S3R_TITEM) && S3R_TITEM
+        // one lane per staged triangle: all its rows in this tile, wy += dy between rows (:378)
+        if (nr) {                                        // nr == 0 beyond the stage
+            const uint32_t k = tid;
+            const uint32_t xmin = ls.xmin[k];
+            const uint32_t x0 = max(xmin, lx0), x1 = min(ls.xmax[k], lx1);
+            float wy[3], d[3], dyv[3], r[3];
+            uint32_t yprev = ls.ymin[k];
+#pragma unroll
+            for (uint32_t c = 0; c < 3; c++) {
+                d[c] = ls.dx[c][k]; dyv[c] = ls.dy[c][k]; r[c] = ls.rz[c][k]; wy[c] = ls.ws[c][k];
+            }
+            const unsigned long long low = 0xFFFFFFFFull - ls.slot[k];
+            for (uint32_t lr = ls.r0[k], lend = lr + nr; lr < lend; lr++) {
+                const uint32_t y = row_of(lr);
+                float w[3];
+#pragma unroll
+                for (uint32_t c = 0; c < 3; c++) {
+                    wy[c] = short_walk(wy[c], dyv[c], y - yprev);
+                    w[c] = short_walk(wy[c], d[c], x0 - xmin);
+                }
+                yprev = y;
+                unsigned long long *krow = ls.key + (lr - tr0) * kKeyStride - lx0;
+                for (uint32_t x = x0; x <= x1; x++) {
+                    if (w[0] >= 0 && w[1] >= 0 && w[2] >= 0) {                        // :362
+                        const float ooz = (r[0] * w[0] + r[1] * w[1]) + r[2] * w[2];  // :363
+                        if (ooz > 0.0f) atomicMax(krow + x, ((unsigned long long)f2u(ooz) << 32) | low);
+                    }
+                    w[0] = w[0] + d[0]; w[1] = w[1] + d[1]; w[2] = w[2] + d[2];    // :374
+                }
+            }
+        }
+        if (items == 0xFFFFFFFFu)
+#endif
         for (uint32_t it = tid; it < items; it += kTileThreads) {
             const uint32_t k = ls.item[it];
             const uint32_t lr = ls.r0[k] + (it - ls.pre[k]);
@@ -1203,7 +1252,7 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
         const float4 *q = reinterpret_cast<const float4 *>(recs + s);
         const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
         const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
-        const uint32_t y = ((lr / band) * nparts + part) * band + lr % band;
+        const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
         const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
         const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
         const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
@@ -1250,8 +1299,25 @@ void stats_read(unsigned long long out[16], bool reset) {
 #ifndef S3R_SEG_PIXELS
 #define S3R_SEG_PIXELS 384
 #endif
-constexpr uint32_t kSegChunks = S3R_SEG_PIXELS / kChunk;   // chunks per fragment segment
+constexpr uint32_t kSegChunks = S3R_SEG_PIXELS / kChunk;   // widest fragment segment, in chunks
 static_assert(kSegChunks * kChunk == S3R_SEG_PIXELS, "segment = whole chunks");
+static_assert(kSegChunks == 6, "k_fragment instantiations below: 6, 3, 2, 1 chunks");
+
+// Segment width of this frame's row path: the widest of 6, 3, 2, 1 chunks that still launches at
+// least kMinFragBlocks workgroups (~20 per CU), so small frames fill the chip (a 1080p frame at
+// 6 chunks is 1350 workgroups; each runs a latency-bound chain, so too few leave CUs idle).
+constexpr uint64_t kMinFragBlocks = 5000;   // measured: 1080p best at 1 chunk (8100 WGs), 4K at 6 (5400 WGs)
+static uint32_t g_segch = kSegChunks;
+
+void fragment_configure(uint32_t W, uint32_t rows_local) {
+    static const uint64_t min_blocks = getenv("S3R_MIN_BLOCKS") ? strtoull(getenv("S3R_MIN_BLOCKS"), nullptr, 10)
+                                                                : kMinFragBlocks;   // tuning override
+    g_segch = 1;
+    for (uint32_t c : {6u, 3u, 2u}) {
+        const uint64_t blocks = (uint64_t)((rows_local + kWaves - 1) / kWaves) * ((W + kChunk * c - 1) / (kChunk * c));
+        if (blocks >= min_blocks) { g_segch = c; break; }
+    }
+}
 
 void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                   const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
@@ -1261,9 +1327,9 @@ void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const
                        m, factor, sw, sh, tris);
 }
 
-uint32_t fragment_segment_pixels() { return kChunk * kSegChunks; }
+uint32_t fragment_segment_pixels() { return kChunk * g_segch; }
 
-uint32_t fragment_segments(uint32_t W) { return (W + kChunk * kSegChunks - 1) / (kChunk * kSegChunks); }
+uint32_t fragment_segments(uint32_t W) { return (W + kChunk * g_segch - 1) / (kChunk * g_segch); }
 
 void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st) {
     if (nslots == 0 || H == 0) return;
@@ -1271,7 +1337,7 @@ void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t
     hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, segs, rowtab);
     if (segs > 1)
         hipLaunchKernelGGL(k_segstart, dim3(nslots, (H + 63) / 64, 3 * ((segs - 1 + 3) / 4)), dim3(64, 4), 0, st,
-                           tris, H, segs, kChunk * kSegChunks, rowtab);
+                           tris, H, segs, kChunk * g_segch, rowtab);
 }
 
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
@@ -1284,7 +1350,7 @@ void launch_bin(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, u
     const uint64_t nb = fragment_bins(W, rows_local);
     if (nb == 0) return;
     hipLaunchKernelGGL(k_bin, dim3((uint32_t)((nb + 3) / 4)), dim3(256), 0, st, tris, nslots, W, H, band, nparts, part,
-                       rows_local, fragment_segments(W), kChunk * kSegChunks, (Entry *)bins, counts);
+                       rows_local, fragment_segments(W), kChunk * g_segch, (Entry *)bins, counts);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
@@ -1293,8 +1359,9 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(k_fragment<kSegChunks>, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab,
-                       tex, ntex, out, W, H, band, nparts, part, segs, rows_local, (const Entry *)bins, counts);
+    auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out, W,
+                       H, band, nparts, part, segs, rows_local, (const Entry *)bins, counts);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

@@ -75,6 +75,9 @@ struct Lib {
     size_t keys_cap = 0;
     uint32_t *tile_total_host = nullptr;       // pinned: (total, appended) per buffer set
     int raster_path = 0;                       // 0 auto, 1 rows (k_bin + k_fragment), 2 tiles
+    bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
+    uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
+    int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[2] = {nullptr, nullptr}, frag_done[2] = {nullptr, nullptr};
     uint32_t parity = 0;
     uint32_t *frame = nullptr;
@@ -222,6 +225,7 @@ void initialize() {
     }
     HIPCHECK(hipSetDevice(g.device));
     if (!g.stream) HIPCHECK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    g.serial = getenv("S3R_SERIAL") != nullptr;
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
     g.vtx = dalloc<float4>(nv); g.nrm = dalloc<float4>(na); g.pay = dalloc<float4>(na);
@@ -360,6 +364,7 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
     const uint32_t p = g.parity;
     g.parity ^= 1u;
     HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
+    if (g.serial) HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p ^ 1u], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
     launch_tile_setup(g.vtx, g.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, g.recs[p],
                       g.boxes[p], g.app_list[p], g.app_count[p], g.tile_counts[p], g.tile_offs[p], g.tile_cursor[p],
@@ -370,6 +375,8 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
     HIPCHECK(hipStreamSynchronize(g.geo));
     const uint32_t napp = host[0];
     const uint64_t total = host[1];
+    g.last_pairs = total;
+    g.last_path = 2;
     if (g.tile_list_cap[p] < total) {
         HIPCHECK(hipDeviceSynchronize());
         if (g.tile_list[p]) HIPCHECK(hipFree(g.tile_list[p]));
@@ -398,7 +405,9 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
         render_tiles(W, H, band, nparts, part, rows_local, out, st, ts);
         return;
     }
+    g.last_path = 1;
     const float sw = (float)W, sh = (float)H;
+    fragment_configure(W, rows_local);
     const size_t need = (size_t)2 * g.ntri * H * (fragment_segments(W) + 1) * 4;
     if (g.rowtab_cap < need) {
         HIPCHECK(hipDeviceSynchronize());
@@ -423,6 +432,7 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     const uint32_t p = g.parity;
     g.parity ^= 1u;
     HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
+    if (g.serial) HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p ^ 1u], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
     launch_setup(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh, g.tris[p], g.geo);
     launch_bin(g.tris[p], 2 * g.ntri, W, H, band, nparts, part, rows_local, g.bins[p], g.bin_counts[p], g.geo);
@@ -537,7 +547,9 @@ __attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
 
 __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
     out[0] = g.nv; out[1] = g.nindices; out[2] = g.na; out[3] = g.ntex; out[4] = 2ull * g.ntri;
-    out[5] = out[6] = out[7] = 0;
+    out[5] = g.last_pairs;                   // tile path: (slot, tile) pairs binned last frame
+    out[6] = (uint64_t)g.last_path;          // fragment stage of the last frame: 1 rows, 2 tiles
+    out[7] = 0;
 }
 
 __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {

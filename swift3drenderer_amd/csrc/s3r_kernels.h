@@ -28,6 +28,8 @@ void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
+// Picks the row path's segment width for a frame of W x rows_local; call before the helpers above.
+void fragment_configure(uint32_t W, uint32_t rows_local);
 
 // Tile path (order-independent fragment stage for many triangles): tiles of 16 local rows x 64 px.
 // recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts/offs/cursor: tile_count().

@@ -14,11 +14,8 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     'base': {},
-    'pre': {'S3R_TPRECHECK': 1},    # plain LDS read before the atomic
+    'st64': {'S3R_TSTAGE': 64},
     'st256': {'S3R_TSTAGE': 256},
-    'tab1': {'S3R_TABLATE': 1},     # setup without tile counting
-    'tab2': {'S3R_TABLATE': 2},     # raster without the LDS atomic
-    'tab4': {'S3R_TABLATE': 4},     # raster without the pixel loop
 }
 
 
@@ -32,7 +29,8 @@ def run():
     extra = shlex.split(os.environ.get('S3R_VARIANT_BENCH', '--scene icosa-stress --pose P_id'))
     out_root = os.path.join(ROOT, 'gpurun_out', 'variants')
     for tag in VARIANTS:
-        env = dict(os.environ, S3R_LIB=os.path.join(ROOT, 'build', f'librender_{tag}.so'), TMPDIR='/tmp')
+        env = dict(os.environ, S3R_LIB=os.path.join(ROOT, 'build', f'librender_{tag}.so'), TMPDIR='/tmp',
+                   S3R_SERIAL='1')
         d = os.path.join(out_root, tag)
         cmd = ['rocprofv3', '--kernel-trace', '--stats', '-d', d, '-o', 'run', '--output-format', 'csv', '--',
                sys.executable, 'bench.py', '--steps', '10', '--warmup', '2', '--no-cpu-baseline', '--no-e2e'] + extra
