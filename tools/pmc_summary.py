@@ -45,11 +45,13 @@ def main():
         print(k)
         for c in sorted(cs):
             print(f'   {c:28s} {cs[c]:.6g}')
-    frag = next((v for k, v in out.items() if 'k_fragment' in k), None)
-    if frag and a.workload and 'FETCH_SIZE' in frag and 'WRITE_SIZE' in frag:
-        t = {a.workload: {'kernel': 'k_fragment', 'fetch_size_kib': frag['FETCH_SIZE'],
-                          'write_size_kib': frag['WRITE_SIZE'],
-                          'hbm_bytes_per_launch': int((2 * frag['FETCH_SIZE'] + frag['WRITE_SIZE']) * 1024),
+    # the fragment stage: k_fragment (row path) or k_tile_raster + k_tile_resolve (tile path)
+    stage = [k for k in out if 'k_fragment' in k] or [k for k in out if 'k_tile_raster' in k or 'k_tile_resolve' in k]
+    if stage and a.workload and all('FETCH_SIZE' in out[k] and 'WRITE_SIZE' in out[k] for k in stage):
+        fetch = sum(out[k]['FETCH_SIZE'] for k in stage)
+        write = sum(out[k]['WRITE_SIZE'] for k in stage)
+        t = {a.workload: {'kernel': '+'.join(k.split('::')[-1] for k in stage), 'fetch_size_kib': fetch,
+                          'write_size_kib': write, 'hbm_bytes_per_launch': int((2 * fetch + write) * 1024),
                           'formula': '(2*FETCH_SIZE + WRITE_SIZE) * 1024, MI355X_MICROARCH.md HBM section'}}
         with open(os.path.join(a.dir, 'pmc_traffic.json'), 'w') as fh:
             json.dump(t, fh, indent=1)
