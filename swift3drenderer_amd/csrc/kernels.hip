@@ -1,9 +1,9 @@
 // kernels.hip -- the gfx950 HIP kernels of the rasterizer.
 //
-//   k_setup     render.cpp:284-359  per triangle: vertex + normal transform of its corners, gather,
-//                                   reject, near-plane clip (:212-262), cull, raster setup.  Writes
-//                                   slot t and, for a clip split, slot T+t.
-//   k_rowstart  render.cpp:374-379  exact row-start / segment-start barycentrics per (slot, row).
+//   k_geometry  render.cpp:284-359, :374-379  per (slot, row block): vertex + normal transform of the
+//                                   slot's corners, reject, near-plane clip (:212-262), cull, raster
+//                                   setup (slot t, or slot T+t for a clip split); the fragment
+//                                   workgroups' slot masks; exact row and segment starts.
 //   k_fragment  render.cpp:360-382  one wave per (row, 64*NCH-pixel segment).  Triangles are taken
 //                                   in slot order, 64 at a time: lanes first act as TRIANGLES and
 //                                   walk each triangle's exact barycentric sequence to this row
@@ -173,17 +173,19 @@ __device__ __forceinline__ void setup_tri(const Vert d[3], bool textured, float 
     *out = t;
 }
 
-// One thread per original triangle; the vertex and normal transforms of its three corners
-// (render.cpp:285-292) are done in place, so the frame needs no camera-space vertex arrays (each
-// corner reads 16 + 16 B instead of writing and re-reading 48 B of transformed data).
-__global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ vtx, const float4 *__restrict__ nrm,
-                                               const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
-                                               const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
-                                               uint32_t ntri, Mat34 m, float factor, float sw, float sh,
-                                               TriSetup *__restrict__ tris) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntri) return;
+// Slot s of the frame's triangle list, set up exactly as the reference's loop meets it
+// (render.cpp:285-359): slot t < T is original triangle t after the :306 reject and the near-plane
+// clip (:308, which may edit it), slot T + t the triangle clip() appended while processing t
+// (:239-257; dead when none).  The vertex and normal transforms of the three corners (:285-292) are
+// done in place, so the frame needs no camera-space vertex arrays.
+__device__ void geo_slot_setup(uint32_t s, uint32_t ntri, const float4 *__restrict__ vtx,
+                               const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
+                               const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx,
+                               const uint32_t *__restrict__ aidx, const Mat34 &m, float factor, float sw, float sh,
+                               TriSetup &out) {
+    const uint32_t t = s < ntri ? s : s - ntri;
     const float half_w = sw / 2, half_h = sh / 2;
+    out.kind = kDead;
     Vert d[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -197,27 +199,25 @@ __global__ void __launch_bounds__(256) k_setup(const float4 *__restrict__ vtx, c
         d[k].pay = pay[ai];
     }
     const bool textured = disc[aidx[3 * t]] != 0;                        // data[0].ca.disc, :340
-    tris[ntri + t].kind = kDead;
-    if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) <= kNear) {         // :306
-        tris[t].kind = kDead;
-        return;
-    }
+    if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) <= kNear) return;  // :306
     Vert app[3];
     uint32_t app_first = 0;
     bool appended = false;
     if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear)            // :308
         appended = clip_tri(d, app, &app_first, textured, factor, half_w, half_h);
-    setup_tri(d, textured, sw, sh, &tris[t]);
-    if (appended) {
+    if (s < ntri) {
+        setup_tri(d, textured, sw, sh, &out);
+    } else if (appended) {
         // The appended triangle is (vi[cur], new, new) with z = (z_cur > near, near, near): neither
         // the :306 reject nor another clip can trigger when the reference loop reaches it.  Its
         // data[0] is the original attribute ai[cur], whose disc picks its colour path.
-        setup_tri(app, disc[aidx[3 * t + app_first]] != 0, sw, sh, &tris[ntri + t]);
+        setup_tri(app, disc[aidx[3 * t + app_first]] != 0, sw, sh, &out);
     }
 }
 
 #ifdef S3R_STATS
 __device__ unsigned long long g_stats[16];
+__device__ unsigned long long g_tstats[8];   // k_geometry wall-clock (100 MHz) profile, stats build
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
     return v;
@@ -226,57 +226,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #else
 #define S3R_IT(p)
 #endif
-
-// ------------------------------------------------------------------ K3: row and segment starts
-// rowtab[((slot * H + y) * (segs + 1) + j) * 4 + c], component c of the exact walk of row y
-// (render.cpp:374-379):  j = 0: at x = xmin, i.e. weight.wy after y - ymin steps of dy;
-// j = 1 + s: at x = s * segw, the first pixel of fragment segment s, for every segment boundary
-// inside (xmin, xmax].  k_rowstart: one lane per (slot, row, component); k_segstart: one lane per
-// (slot, row, component, segment boundary), each walking from the row start -- so the critical
-// path is one row walk plus one partial-row walk.
-__global__ void __launch_bounds__(192) k_rowstart(const TriSetup *__restrict__ tris, uint32_t H, uint32_t segs,
-                                                  float *__restrict__ rowtab) {
-    const uint32_t slot = blockIdx.x;
-    const uint32_t y = blockIdx.y * 64u + threadIdx.x;
-    const uint32_t c = threadIdx.y;
-    const TriSetup *t = tris + slot;
-    const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
-    if (h0.x == kDead) return;
-    const uint32_t ymax = reinterpret_cast<const uint4 *>(t)[1].x;
-    if (y < h0.w || y > ymax || y >= H) return;
-#ifdef S3R_STATS
-    uint32_t it_row = 0;
-    rowtab[((size_t)slot * H + y) * (segs + 1) * 4 + c] = exact_walk(t->ws[c], t->dy[c], y - h0.w, &it_row);
-    atomicAdd(&g_stats[12], (unsigned long long)it_row);
-    atomicMax(&g_stats[13], (unsigned long long)it_row);
-#else
-    rowtab[((size_t)slot * H + y) * (segs + 1) * 4 + c] = exact_walk(t->ws[c], t->dy[c], y - h0.w);
-#endif
-}
-
-__global__ void __launch_bounds__(256) k_segstart(const TriSetup *__restrict__ tris, uint32_t H, uint32_t segs,
-                                                  uint32_t segw, float *__restrict__ rowtab) {
-    const uint32_t slot = blockIdx.x;
-    const uint32_t y = blockIdx.y * 64u + threadIdx.x;
-    const uint32_t c = blockIdx.z % 3u;
-    const uint32_t sg = (blockIdx.z / 3u) * 4u + threadIdx.y + 1u;      // boundaries 1 .. segs-1
-    const TriSetup *t = tris + slot;
-    const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
-    if (h0.x == kDead) return;
-    const uint32_t ymax = reinterpret_cast<const uint4 *>(t)[1].x;
-    if (y < h0.w || y > ymax || y >= H || sg >= segs) return;
-    const uint32_t xb = sg * segw;
-    if (xb <= h0.y || xb > h0.z) return;
-    float *row = rowtab + ((size_t)slot * H + y) * (segs + 1) * 4 + c;
-#ifdef S3R_STATS
-    uint32_t it = 0;
-    row[(1 + sg) * 4] = exact_walk(row[0], t->dx[c], xb - h0.y, &it);
-    atomicAdd(&g_stats[14], (unsigned long long)it);
-    atomicMax(&g_stats[15], (unsigned long long)it);
-#else
-    row[(1 + sg) * 4] = exact_walk(row[0], t->dx[c], xb - h0.y);
-#endif
-}
 
 // ------------------------------------------------------------------ ripmap sample
 __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t base,
@@ -374,6 +323,23 @@ S3R_CALLEE float walk(float s, float d, uint32_t n
 }
 
 
+// All waves copy the raster constants of the listed slots (sh.ent[i].slot, i < cnt) into LDS.
+__device__ __forceinline__ void load_entries(const TriSetup *__restrict__ tris, FragShared &sh, uint32_t cnt,
+                                             uint32_t wave, uint32_t lane) {
+    for (uint32_t i = wave * 64 + lane; i < cnt; i += kWaves * 64) {
+        const TriSetup *t = tris + sh.ent[i].slot;
+        const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
+        const uint4 h1 = reinterpret_cast<const uint4 *>(t)[1];
+        const float4 dx = reinterpret_cast<const float4 *>(t)[3];
+        const float4 rz = reinterpret_cast<const float4 *>(t)[5];
+        Entry &e = sh.ent[i];
+        e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
+        e.dx[0] = dx.x; e.dx[1] = dx.y; e.dx[2] = dx.z;
+        e.rvz[0] = rz.x; e.rvz[1] = rz.y; e.rvz[2] = rz.z;
+    }
+    __syncthreads();
+}
+
 // Wave 0 lists, in slot order, the live triangles whose bbox meets rows [y0, y1] and columns
 // [x0, x1], starting at slot `cursor`, at most kListMax; then all waves copy each listed triangle's
 // raster constants into LDS.  Must be reached by every wave of the workgroup.
@@ -410,70 +376,102 @@ __device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, u
         if (lane == 0) { sh.cnt = cnt; sh.next = cursor < nslots ? cursor : nslots; }
     }
     __syncthreads();
-    const uint32_t cnt = sh.cnt;
-    for (uint32_t i = wave * 64 + lane; i < cnt; i += kWaves * 64) {
-        const TriSetup *t = tris + sh.ent[i].slot;
-        const uint4 h0 = reinterpret_cast<const uint4 *>(t)[0];
-        const uint4 h1 = reinterpret_cast<const uint4 *>(t)[1];
-        const float4 dx = reinterpret_cast<const float4 *>(t)[3];
-        const float4 rz = reinterpret_cast<const float4 *>(t)[5];
-        Entry &e = sh.ent[i];
-        e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
-        e.dx[0] = dx.x; e.dx[1] = dx.y; e.dx[2] = dx.z;
-        e.rvz[0] = rz.x; e.rvz[1] = rz.y; e.rvz[2] = rz.z;
-    }
-    __syncthreads();
+    load_entries(tris, sh, sh.cnt, wave, lane);
 }
 
-// ------------------------------------------------------------------ K4a: binning
-// One wave per bin = (block of kWaves local rows) x (fragment segment): the live triangles whose
-// bbox meets it, in slot order (the reference's processing order), written as compact Entry records
-// so the fragment workgroup loads its list with one coalesced read.  counts[bin] = kListMax + 1
-// marks an overflowing bin: the fragment kernel then scans the slots itself, in rounds.
-__global__ void __launch_bounds__(256) k_bin(const TriSetup *__restrict__ tris, uint32_t nslots, uint32_t W,
-                                             uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                                             uint32_t rows_local, uint32_t segs, uint32_t segw,
-                                             Entry *__restrict__ bins, uint32_t *__restrict__ counts) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t bin = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t nblk = (rows_local + kWaves - 1) / kWaves;
-    if (bin >= nblk * segs) return;
-    const uint32_t blk = bin / segs, seg = bin - blk * segs;
-    uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
-    for (uint32_t k = 0; k < kWaves && blk * kWaves + k < rows_local; k++) {
-        const uint32_t lr = blk * kWaves + k;
-        const uint32_t yy = ((lr / band) * nparts + part) * band + lr % band;
-        y0 = min(y0, yy); y1 = max(y1, yy);
+// ------------------------------------------------------------------ K1: geometry, one launch
+// Per frame, on the geometry stream (overlapping the previous frame's fragment kernel): one
+// workgroup per (slot, block of kGeoRows local rows) x 3 components.
+//   * thread 0 sets the slot up (geo_slot_setup: transform, reject, clip, cull, raster setup,
+//     render.cpp:285-359); the row-block-0 workgroup stores the slot's TriSetup record;
+//   * bins: the slot's bit is set in the slot mask of every fragment workgroup (kWaves local rows x
+//     one segment) its bbox meets -- the fragment kernel reads the set bits in slot order, i.e. the
+//     reference's processing order, and clears them for the buffer's next frame;
+//   * starts: lane (row, component) walks the reference's sequence exactly (exact_walk): wy += dy
+//     down to its row (render.cpp:378), then w += dx along the row through every fragment-segment
+//     boundary inside the bbox (:374), storing the row start and each segment start.
+// rowtab[((slot * rows_local + lr) * (segs + 1) + j) * 4 + c]: j = 0 at x = xmin, j = 1 + s at
+// x = s * segw (only boundaries in (xmin, xmax] are written).
+constexpr uint32_t kGeoRows = 128;
+static_assert(kGeoRows % kWaves == 0, "geometry row blocks hold whole fragment row blocks");
+
+__global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
+    const float4 *__restrict__ vtx, const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
+    const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
+    uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+    uint32_t rows_local, uint32_t segs, uint32_t segw, uint32_t nwords, TriSetup *__restrict__ tris,
+    float *__restrict__ rowtab, uint32_t *__restrict__ binmask) {
+    __shared__ TriSetup sts;
+    const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
+#ifdef S3R_STATS
+    const unsigned long long t_start = wall_clock64();
+    if (tid == 0) atomicMin(&g_tstats[2], t_start);
+#endif
+    if (tid == 0) {
+        TriSetup t;
+        geo_slot_setup(slot, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, (float)W, (float)H, t);
+        sts = t;
+        if (rb == 0) tris[slot] = t;
+#ifdef S3R_STATS
+        atomicMax(&g_tstats[0], wall_clock64() - t_start);
+#endif
     }
-    const uint32_t x0 = seg * segw, x1 = min(W, x0 + segw) - 1u;
-    Entry *out = bins + (size_t)bin * kListMax;
-    uint32_t cnt = 0;
-    bool over = false;
-    for (uint32_t cursor = 0; cursor < nslots && !over; cursor += 64u) {
-        const uint32_t s = cursor + lane;
-        bool act = false;
-        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
-        if (s < nslots) {
-            h0 = reinterpret_cast<const uint4 *>(tris + s)[0];                   // kind xmin xmax ymin
-            h1 = reinterpret_cast<const uint4 *>(tris + s)[1];                   // ymax ...
-            act = h0.x != kDead && h0.w <= y1 && h1.x >= y0 && h0.y <= x1 && h0.z >= x0 && y0 < H;
+    __syncthreads();
+    if (sts.kind == kDead) return;
+    const uint32_t xmin = sts.xmin, xmax = sts.xmax, ymin = sts.ymin, ymax = sts.ymax;
+    auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
+
+    // bins of this workgroup's rows: (kGeoRows / kWaves) fragment row blocks x segs segments
+    const uint32_t nbr = kGeoRows / kWaves;
+    for (uint32_t q = tid; q < nbr * segs; q += 3 * kGeoRows) {
+        const uint32_t blk = rb * nbr + q / segs, sg = q % segs;
+        const uint32_t lr0 = blk * kWaves;
+        if (lr0 >= rows_local) continue;
+        uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
+        for (uint32_t k = 0; k < kWaves && lr0 + k < rows_local; k++) {
+            const uint32_t yy = row_of(lr0 + k);
+            y0 = min(y0, yy); y1 = max(y1, yy);
         }
-        const uint64_t mask = __ballot(act);
-        const uint32_t pc = (uint32_t)__builtin_popcountll(mask);
-        if (cnt + pc > kListMax) { over = true; break; }
-        if (act) {
-            const float4 dx = reinterpret_cast<const float4 *>(tris + s)[3];
-            const float4 rz = reinterpret_cast<const float4 *>(tris + s)[5];
-            Entry e;
-            e.slot = s; e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
-            e.dx[0] = dx.x; e.dx[1] = dx.y; e.dx[2] = dx.z;
-            e.rvz[0] = rz.x; e.rvz[1] = rz.y; e.rvz[2] = rz.z;
-            e.pad = 0;
-            out[cnt + lane_prefix(mask, lane)] = e;
-        }
-        cnt += pc;
+        const uint32_t x0 = sg * segw, x1 = min(W, x0 + segw) - 1u;
+        if (ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)
+            atomicOr(&binmask[((size_t)blk * segs + sg) * nwords + (slot >> 5)], 1u << (slot & 31u));
     }
-    if (lane == 0) counts[bin] = over ? kListMax + 1u : cnt;
+
+    // exact row and segment starts
+    const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
+    if (lr >= rows_local) return;
+    const uint32_t y = row_of(lr);
+    if (y < ymin || y > ymax || y >= H) return;
+    float *row = rowtab + ((size_t)slot * rows_local + lr) * (segs + 1) * 4 + c;
+    const float d = sts.dx[c];
+#ifdef S3R_STATS
+    uint32_t it_row = 0, it_seg = 0;
+    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin, &it_row);
+#else
+    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
+#endif
+    row[0] = v;
+    uint32_t xp = xmin;
+    for (uint32_t sg = xmin / segw + 1u; sg < segs; sg++) {
+        const uint32_t xb = sg * segw;
+        if (xb > xmax) break;
+#ifdef S3R_STATS
+        v = exact_walk(v, d, xb - xp, &it_seg);
+#else
+        v = exact_walk(v, d, xb - xp);
+#endif
+        xp = xb;
+        row[(1 + sg) * 4] = v;
+    }
+#ifdef S3R_STATS
+    const unsigned long long t_end = wall_clock64();
+    atomicMax(&g_tstats[1], t_end - t_start);
+    atomicMax(&g_tstats[3], t_end);
+    atomicAdd(&g_stats[12], (unsigned long long)it_row);
+    atomicMax(&g_stats[13], (unsigned long long)it_row);
+    atomicAdd(&g_stats[14], (unsigned long long)it_seg);
+    atomicMax(&g_stats[15], (unsigned long long)it_seg);
+#endif
 }
 
 // Deferred shading of the winning triangle (render.cpp:366-371).
@@ -633,8 +631,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
-                                                  uint32_t rows_local, const Entry *__restrict__ bins,
-                                                  const uint32_t *__restrict__ counts) {
+                                                  uint32_t rows_local, uint32_t *__restrict__ binmask,
+                                                  uint32_t nwords) {
     __shared__ FragShared sh;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t blk = blockIdx.x / segs, seg = blockIdx.x - blk * segs;
@@ -658,23 +656,36 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     uint32_t *p_chunk = &st_chunk, *p_pix = &st_pix;
 #endif
 
-    // this workgroup's triangle list, binned by k_bin (one coalesced read), or, for an overflowing
-    // bin, the first round of an in-kernel slot scan
-    const uint32_t bcount = counts[blockIdx.x];
+    // this workgroup's triangle list: the set bits of its slot mask (k_geometry), in slot order --
+    // or, beyond kListMax triangles, the first round of an in-kernel slot scan
     bool overflow;
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 32)
-    if (bcount <= kListMax + 100u) {      // ablation: no list load (garbage list, count forced to 0)
-        if (threadIdx.x == 0) sh.cnt = 0u * bcount;
-        __syncthreads();
-        overflow = false;
-    } else
-#endif
-    if (bcount <= kListMax) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(bins + (size_t)blockIdx.x * kListMax);
-        uint4 *dst = reinterpret_cast<uint4 *>(sh.ent);
-        for (uint32_t i = threadIdx.x; i < bcount * 3u; i += 64u * kWaves) dst[i] = src[i];
-        if (threadIdx.x == 0) sh.cnt = bcount;
-        __syncthreads();
+    if (wave == 0) {
+        uint32_t *mw = binmask + (size_t)blockIdx.x * nwords;
+        uint32_t cnt = 0;
+        for (uint32_t base = 0; base < nwords; base += 64u) {
+            const uint32_t i = base + lane;
+            uint32_t w = i < nwords ? mw[i] : 0u;
+            if (w) mw[i] = 0u;                                   // cleared for the buffer's next frame
+            const uint32_t pc = (uint32_t)__builtin_popcount(w);
+            uint32_t inc = pc;
+            for (uint32_t o = 1; o < 64u; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+                if (lane >= o) inc += v;
+            }
+            uint32_t pos = cnt + inc - pc;
+            while (w) {
+                const uint32_t b = (uint32_t)__builtin_ctz(w);
+                w &= w - 1u;
+                if (pos < kListMax) sh.ent[pos].slot = i * 32u + b;
+                pos++;
+            }
+            cnt += rdl(inc, 63u);
+        }
+        if (lane == 0) sh.cnt = cnt;
+    }
+    __syncthreads();
+    if (sh.cnt <= kListMax) {
+        load_entries(tris, sh, sh.cnt, wave, lane);
         overflow = false;
     } else {
         build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
@@ -695,7 +706,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                     // exact value AT this triangle's first pixel in the segment (xmin, or the
                     // segment start): the first chunk then needs no walking at all
                     const bool inside = e.xmin >= xs;
-                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * H + y) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
+                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * rows_local + lr) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
                     st_k[b * 64 + lane] = inside ? e.xmin : xs;
                 }
             }
@@ -809,7 +820,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                             v.c = v.k0 == kp ? cp : (v.k0 == kp + 1u ? cp + v.d : walk(cp, v.d, v.k0 - kp S3R_IT(p_chunk)));
                         } else {
                             const bool inside = e.xmin >= xs;
-                            const float c0v = rowtab[(((size_t)e.slot * H + y) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
+                            const float c0v = rowtab[(((size_t)e.slot * rows_local + lr) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
                             v.c = walk(c0v, v.d, v.k0 - (inside ? e.xmin : xs) S3R_IT(p_chunk));
                         }
                         v.lin = chunk_linear(v.c, v.d, v.m, &v.del);
@@ -1281,17 +1292,20 @@ void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *
     hipLaunchKernelGGL(k_walk_test, dim3((count + 255) / 256), dim3(256), 0, st, s, d, n, out, lin, del, count);
 }
 
-void stats_read(unsigned long long out[16], bool reset) {
+void stats_read(unsigned long long out[24], bool reset) {
 #ifdef S3R_STATS
     (void)hipDeviceSynchronize();
     (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stats), sizeof(unsigned long long) * 16, 0, hipMemcpyDeviceToHost);
+    (void)hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_tstats), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost);
     if (reset) {
         unsigned long long z[16] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stats), z, sizeof z, 0, hipMemcpyHostToDevice);
+        z[2] = ~0ull;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tstats), z, sizeof(unsigned long long) * 8, 0, hipMemcpyHostToDevice);
     }
 #else
     (void)reset;
-    for (int i = 0; i < 16; i++) out[i] = 0;
+    for (int i = 0; i < 24; i++) out[i] = 0;
 #endif
 }
 
@@ -1319,49 +1333,34 @@ void fragment_configure(uint32_t W, uint32_t rows_local) {
     }
 }
 
-void launch_setup(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
-                  const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
-                  float sw, float sh, TriSetup *tris, hipStream_t st) {
-    if (ntri == 0) return;
-    hipLaunchKernelGGL(k_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, nrm, pay, disc, vidx, aidx, ntri,
-                       m, factor, sw, sh, tris);
-}
-
 uint32_t fragment_segment_pixels() { return kChunk * g_segch; }
 
 uint32_t fragment_segments(uint32_t W) { return (W + kChunk * g_segch - 1) / (kChunk * g_segch); }
 
-void launch_rowstart(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, float *rowtab, hipStream_t st) {
-    if (nslots == 0 || H == 0) return;
-    const uint32_t segs = fragment_segments(W);
-    hipLaunchKernelGGL(k_rowstart, dim3(nslots, (H + 63) / 64), dim3(64, 3), 0, st, tris, H, segs, rowtab);
-    if (segs > 1)
-        hipLaunchKernelGGL(k_segstart, dim3(nslots, (H + 63) / 64, 3 * ((segs - 1 + 3) / 4)), dim3(64, 4), 0, st,
-                           tris, H, segs, kChunk * g_segch, rowtab);
-}
-
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
     return (uint64_t)((rows_local + kWaves - 1) / kWaves) * fragment_segments(W);
 }
-size_t bin_entry_bytes() { return sizeof(Entry) * kListMax; }
+uint32_t bin_words(uint32_t nslots) { return (nslots + 31u) / 32u; }
 
-void launch_bin(const TriSetup *tris, uint32_t nslots, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
-                uint32_t part, uint32_t rows_local, void *bins, uint32_t *counts, hipStream_t st) {
-    const uint64_t nb = fragment_bins(W, rows_local);
-    if (nb == 0) return;
-    hipLaunchKernelGGL(k_bin, dim3((uint32_t)((nb + 3) / 4)), dim3(256), 0, st, tris, nslots, W, H, band, nparts, part,
-                       rows_local, fragment_segments(W), kChunk * g_segch, (Entry *)bins, counts);
+void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
+                     const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
+                     uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st) {
+    if (ntri == 0 || rows_local == 0) return;
+    hipLaunchKernelGGL(k_geometry, dim3(2 * ntri, (rows_local + kGeoRows - 1) / kGeoRows), dim3(3 * kGeoRows), 0, st,
+                       vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band, nparts, part, rows_local,
+                       fragment_segments(W), kChunk * g_segch, bin_words(2 * ntri), tris, rowtab, binmask);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, const void *bins, const uint32_t *counts, hipStream_t st) {
+                     uint32_t rows_local, uint32_t *binmask, hipStream_t st) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) return;
     auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out, W,
-                       H, band, nparts, part, segs, rows_local, (const Entry *)bins, counts);
+                       H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots));
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -36,6 +37,12 @@ namespace {
 
 struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
 
+// Per-frame buffer sets in flight: frame k's geometry writes set k % kSets once the fragment kernel
+// of frame k - kSets (the set's last reader) is done, on geometry stream k % kGeoStreams, so the
+// geometry of two consecutive frames and the previous frame's fragment kernel can all overlap.
+constexpr int kSets = 3;
+constexpr int kGeoStreams = 2;
+
 struct Lib {
     bool initialized = false;
     std::string data_path;     // "" = reference search
@@ -55,34 +62,33 @@ struct Lib {
     float4 *vtx = nullptr, *nrm = nullptr, *pay = nullptr;
     uint8_t *disc = nullptr;
     uint32_t *vidx = nullptr, *aidx = nullptr, *tex = nullptr;
-    // per-frame geometry, double-buffered: frame k's geometry (k_setup, k_rowstart on stream `geo`)
-    // overlaps frame k-1's fragment kernel on the caller's stream
-    TriSetup *tris[2] = {nullptr, nullptr};
-    float *rowtab[2] = {nullptr, nullptr};     // 2T x H x (segments + 1) x float4 exact row starts
+    // per-frame geometry, double-buffered: frame k's geometry (k_geometry on stream `geo`) overlaps
+    // frame k-1's fragment kernel on the caller's stream
+    TriSetup *tris[kSets] = {};
+    float *rowtab[kSets] = {};     // 2T x rows x (segments + 1) x float4 exact row starts
     size_t rowtab_cap = 0;
-    void *bins[2] = {nullptr, nullptr};        // per-workgroup triangle lists (k_bin)
-    uint32_t *bin_counts[2] = {nullptr, nullptr};
-    uint64_t bins_cap = 0;
+    uint32_t *binmask[kSets] = {}; // per fragment workgroup: slot mask (zero between frames)
+    uint64_t binmask_cap = 0;
     // tile path (many triangles): per-tile counts, offsets, scatter cursors, slot lists
-    uint32_t *tile_counts[2] = {nullptr, nullptr}, *tile_offs[2] = {nullptr, nullptr};
-    uint32_t *tile_cursor[2] = {nullptr, nullptr}, *tile_total[2] = {nullptr, nullptr};
-    uint32_t *tile_list[2] = {nullptr, nullptr};
-    void *recs[2] = {nullptr, nullptr};        // 2T raster records (positions-only setup)
-    uint32_t *boxes[2] = {nullptr, nullptr};   // T packed bboxes
-    uint32_t *app_list[2] = {nullptr, nullptr}, *app_count[2] = {nullptr, nullptr};
-    uint64_t tiles_cap = 0, tile_list_cap[2] = {0, 0};
+    uint32_t *tile_counts[kSets] = {}, *tile_offs[kSets] = {};
+    uint32_t *tile_cursor[kSets] = {}, *tile_total[kSets] = {};
+    uint32_t *tile_list[kSets] = {};
+    void *recs[kSets] = {};        // 2T raster records (positions-only setup)
+    uint32_t *boxes[kSets] = {};   // T packed bboxes
+    uint32_t *app_list[kSets] = {}, *app_count[kSets] = {};
+    uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
     uint32_t *tile_total_host = nullptr;       // pinned: (total, appended) per buffer set
-    int raster_path = 0;                       // 0 auto, 1 rows (k_bin + k_fragment), 2 tiles
+    int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
-    hipEvent_t geo_done[2] = {nullptr, nullptr}, frag_done[2] = {nullptr, nullptr};
-    uint32_t parity = 0;
+    hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
+    uint32_t frame_no = 0;                     // frames issued: set frame_no % kSets
     uint32_t *frame = nullptr;
     size_t frame_cap = 0;
-    hipStream_t stream = nullptr, geo = nullptr;
+    hipStream_t stream = nullptr, geo[kGeoStreams] = {};
 
     // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
     struct Reg { void *p; size_t n; bool ok; };
@@ -94,6 +100,27 @@ struct Lib {
 };
 
 Lib g;
+
+// S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
+struct HostProf {
+    bool on = getenv("S3R_HOSTPROF") != nullptr;
+    double t[6] = {};
+    uint64_t frames = 0;
+    std::chrono::steady_clock::time_point last;
+    void start() { if (on) last = std::chrono::steady_clock::now(); }
+    void lap(int i) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        t[i] += std::chrono::duration<double, std::micro>(now - last).count();
+        last = now;
+    }
+    void report() {
+        if (!on || !frames) return;
+        fprintf(stderr, "s3r hostprof (us/frame over %llu): begin %.2f  prep %.2f  geo-wait %.2f  geo-launch %.2f  "
+                "frag-wait %.2f  frag-launch %.2f\n", (unsigned long long)frames, t[0] / frames, t[1] / frames,
+                t[2] / frames, t[3] / frames, t[4] / frames, t[5] / frames);
+    }
+} hp;
 
 float config_scale() {
     const float fov = (float)M_PI / 5.f;        // render.cpp:91
@@ -232,12 +259,17 @@ void initialize() {
     g.disc = dalloc<uint8_t>(na);
     g.vidx = dalloc<uint32_t>(3 * ntri); g.aidx = dalloc<uint32_t>(3 * ntri);
     g.tex = dalloc<uint32_t>(nt);
-    for (int p = 0; p < 2; p++) {
+    for (int p = 0; p < kSets; p++) {
         g.tris[p] = dalloc<TriSetup>(2 * ntri);
         HIPCHECK(hipEventCreateWithFlags(&g.geo_done[p], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&g.frag_done[p], hipEventDisableTiming));
     }
-    if (!g.geo) HIPCHECK(hipStreamCreateWithFlags(&g.geo, hipStreamNonBlocking));
+    // geometry streams at the highest priority: their (small, latency-bound) workgroups are
+    // dispatched as soon as the previous frame's fragment workgroups free a slot
+    int prio_least = 0, prio_greatest = 0;
+    HIPCHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    for (hipStream_t &gs : g.geo)
+        if (!gs) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
     HIPCHECK(hipMemcpy(g.vtx, vtx.data(), nv * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(g.nrm, nrm.data(), na * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(g.pay, pay.data(), na * 16, hipMemcpyHostToDevice));
@@ -257,11 +289,12 @@ void release_all() {
     if (g.initialized) {
         (void)hipSetDevice(g.device);
         if (g.stream) (void)hipStreamSynchronize(g.stream);
-        if (g.geo) (void)hipStreamSynchronize(g.geo);
+        for (hipStream_t gs : g.geo)
+            if (gs) (void)hipStreamSynchronize(gs);
         (void)hipDeviceSynchronize();
         unregister_all();
         void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.tris[0], g.tris[1], g.frame,
-                        g.rowtab[0], g.rowtab[1], g.bins[0], g.bins[1], g.bin_counts[0], g.bin_counts[1],
+                        g.rowtab[0], g.rowtab[1], g.binmask[0], g.binmask[1],
                         g.tile_counts[0], g.tile_counts[1], g.tile_offs[0], g.tile_offs[1], g.tile_cursor[0],
                         g.tile_cursor[1], g.tile_list[0], g.tile_list[1],  // tile_total aliases app_count
                         g.recs[0], g.recs[1], g.boxes[0], g.boxes[1], g.app_list[0], g.app_list[1],
@@ -269,11 +302,12 @@ void release_all() {
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
         if (g.tile_total_host) (void)hipHostFree(g.tile_total_host);
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < kSets; p++) {
             if (g.geo_done[p]) (void)hipEventDestroy(g.geo_done[p]);
             if (g.frag_done[p]) (void)hipEventDestroy(g.frag_done[p]);
         }
-        if (g.geo) (void)hipStreamDestroy(g.geo);
+        for (hipStream_t gs : g.geo)
+            if (gs) (void)hipStreamDestroy(gs);
         for (auto &t : g.tslots) {
             (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
         }
@@ -316,6 +350,17 @@ TimingSlot *timing_slot() {
     return &g.tslots[g.tcount++];
 }
 
+// The buffer set of the frame being issued; frames cycle through kSets sets.
+uint32_t next_set() {
+    g.frame_no++;
+    return g.frame_no % kSets;
+}
+
+// S3R_SERIAL (profiling): the geometry waits for every earlier fragment kernel -- no overlap.
+void wait_all_fragments(hipStream_t geo) {
+    for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[q], 0));
+}
+
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
 // the order-independent tile path takes over (the icosahedron stress scene).
 constexpr uint64_t kRowPathMaxSlots = 8192;
@@ -336,7 +381,7 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
     const uint64_t nt = tile_count(W, rows_local);
     if (g.tiles_cap < nt) {
         HIPCHECK(hipDeviceSynchronize());
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < kSets; p++) {
             for (uint32_t **q : {&g.tile_counts[p], &g.tile_offs[p], &g.tile_cursor[p]}) {
                 if (*q) HIPCHECK(hipFree(*q));
                 *q = dalloc<uint32_t>(nt);
@@ -352,27 +397,27 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
         g.keys_cap = npx;
     }
     if (!g.recs[0]) {
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < kSets; p++) {
             g.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
             g.boxes[p] = dalloc<uint32_t>((size_t)2 * g.ntri);
             g.app_list[p] = dalloc<uint32_t>(g.ntri);
             g.app_count[p] = dalloc<uint32_t>(2);          // [0] appended count, [1] tile-pair total
             g.tile_total[p] = g.app_count[p] + 1;
         }
-        HIPCHECK(hipHostMalloc((void **)&g.tile_total_host, 4 * sizeof(uint32_t)));
+        HIPCHECK(hipHostMalloc((void **)&g.tile_total_host, 2 * kSets * sizeof(uint32_t)));
     }
-    const uint32_t p = g.parity;
-    g.parity ^= 1u;
-    HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
-    if (g.serial) HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p ^ 1u], 0));
-    if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
+    const uint32_t p = next_set();
+    hipStream_t geo = g.geo[0];
+    HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
+    if (g.serial) wait_all_fragments(geo);
+    if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     launch_tile_setup(g.vtx, g.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, g.recs[p],
                       g.boxes[p], g.app_list[p], g.app_count[p], g.tile_counts[p], g.tile_offs[p], g.tile_cursor[p],
-                      g.tile_total[p], g.geo);
+                      g.tile_total[p], geo);
     // the list size is data-dependent: read it back (the tile path's one host sync per frame)
     uint32_t *host = g.tile_total_host + 2 * p;
-    HIPCHECK(hipMemcpyAsync(host, g.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, g.geo));
-    HIPCHECK(hipStreamSynchronize(g.geo));
+    HIPCHECK(hipMemcpyAsync(host, g.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
+    HIPCHECK(hipStreamSynchronize(geo));
     const uint32_t napp = host[0];
     const uint64_t total = host[1];
     g.last_pairs = total;
@@ -385,8 +430,8 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
         g.tile_list_cap[p] = cap;
     }
     launch_tile_fill(g.boxes[p], g.ntri, g.recs[p], g.app_list[p], napp, W, band, nparts, part, g.tile_cursor[p],
-                     g.tile_list[p], g.geo);
-    HIPCHECK(hipEventRecord(g.geo_done[p], g.geo));
+                     g.tile_list[p], geo);
+    HIPCHECK(hipEventRecord(g.geo_done[p], geo));
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_tile_raster(g.recs[p], W, band, nparts, part, rows_local, g.tile_offs[p], g.tile_counts[p], g.tile_list[p],
@@ -406,46 +451,49 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
         return;
     }
     g.last_path = 1;
-    const float sw = (float)W, sh = (float)H;
     fragment_configure(W, rows_local);
-    const size_t need = (size_t)2 * g.ntri * H * (fragment_segments(W) + 1) * 4;
+    const size_t need = (size_t)2 * g.ntri * rows_local * (fragment_segments(W) + 1) * 4;
     if (g.rowtab_cap < need) {
         HIPCHECK(hipDeviceSynchronize());
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < kSets; p++) {
             if (g.rowtab[p]) HIPCHECK(hipFree(g.rowtab[p]));
             g.rowtab[p] = dalloc<float>(need);
         }
         g.rowtab_cap = need;
     }
-    const uint64_t nbins = fragment_bins(W, rows_local);
-    if (g.bins_cap < nbins) {
+    const uint64_t nmask = fragment_bins(W, rows_local) * bin_words(2 * g.ntri);
+    if (g.binmask_cap < nmask) {
         HIPCHECK(hipDeviceSynchronize());
-        for (int p = 0; p < 2; p++) {
-            if (g.bins[p]) HIPCHECK(hipFree(g.bins[p]));
-            if (g.bin_counts[p]) HIPCHECK(hipFree(g.bin_counts[p]));
-            g.bins[p] = dalloc<uint8_t>(nbins * bin_entry_bytes());
-            g.bin_counts[p] = dalloc<uint32_t>(nbins);
+        for (int p = 0; p < kSets; p++) {
+            if (g.binmask[p]) HIPCHECK(hipFree(g.binmask[p]));
+            g.binmask[p] = dalloc<uint32_t>(nmask);
+            HIPCHECK(hipMemset(g.binmask[p], 0, nmask * sizeof(uint32_t)));   // then kept zero by k_fragment
         }
-        g.bins_cap = nbins;
+        g.binmask_cap = nmask;
     }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
-    const uint32_t p = g.parity;
-    g.parity ^= 1u;
-    HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p], 0));
-    if (g.serial) HIPCHECK(hipStreamWaitEvent(g.geo, g.frag_done[p ^ 1u], 0));
-    if (ts) HIPCHECK(hipEventRecord(ts->frame0, g.geo));
-    launch_setup(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh, g.tris[p], g.geo);
-    launch_bin(g.tris[p], 2 * g.ntri, W, H, band, nparts, part, rows_local, g.bins[p], g.bin_counts[p], g.geo);
-    launch_rowstart(g.tris[p], 2 * g.ntri, W, H, g.rowtab[p], g.geo);
-    HIPCHECK(hipEventRecord(g.geo_done[p], g.geo));
+    const uint32_t p = next_set();
+    hipStream_t geo = g.geo[g.frame_no % kGeoStreams];
+    hp.lap(1);
+    HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
+    if (g.serial) wait_all_fragments(geo);
+    if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
+    hp.lap(2);
+    launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
+                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], geo);
+    hp.lap(3);
+    HIPCHECK(hipEventRecord(g.geo_done[p], geo));
     // fragment on the caller's stream
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
+    hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.bins[p], g.bin_counts[p], st);
+                    g.binmask[p], st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(g.frag_done[p], st));
     HIPCHECK(hipGetLastError());
+    hp.lap(5);
+    hp.frames++;
 }
 
 bool host_pinned(void *p, size_t n) {
@@ -491,7 +539,10 @@ __attribute__((visibility("default"))) int s3r_configure(const char *data_path, 
     return 0;
 }
 
-__attribute__((visibility("default"))) void s3r_shutdown(void) { release_all(); }
+__attribute__((visibility("default"))) void s3r_shutdown(void) {
+    hp.report();
+    release_all();
+}
 
 __attribute__((visibility("default"))) int s3r_set_raster_path(int mode) {
     if (mode < 0 || mode > 2) return -1;
@@ -516,7 +567,9 @@ __attribute__((visibility("default"))) int64_t s3r_render_bands(const Input *inp
                                                                uint32_t band_rows, uint32_t n_parts, uint32_t part,
                                                                uint32_t *dev_out, void *stream) {
     if (band_rows == 0 || n_parts == 0 || part >= n_parts || (!dev_out && width && height)) return -1;
+    hp.start();
     frame_begin(input, width, height);
+    hp.lap(0);
     const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
     // NULL is the legacy default (null) stream -- e.g. torch's default stream -- never our own.
     hipStream_t st = (hipStream_t)stream;
@@ -561,9 +614,17 @@ __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], flo
 // (sum over lanes, sum over waves of the wave maximum) for row-walk, chunk-walk and per-pixel walker
 // iterations, irregular chunk components, pixel-triangle tests and triangle batches.
 __attribute__((visibility("default"))) void s3r_stats(uint64_t out[16], int reset) {
-    unsigned long long tmp[16];
+    unsigned long long tmp[24];
     stats_read(tmp, reset != 0);
     for (int i = 0; i < 16; i++) out[i] = tmp[i];
+}
+
+// Stats build only: k_geometry wall-clock profile (100 MHz ticks): {max setup time of a workgroup,
+// max workgroup time, first start, last end, 0...}.  Reset together with s3r_stats(.., 1).
+__attribute__((visibility("default"))) void s3r_stats_geometry(uint64_t out[8]) {
+    unsigned long long tmp[24];
+    stats_read(tmp, false);
+    for (int i = 0; i < 8; i++) out[i] = tmp[16 + i];
 }
 
 // ---- self-test hooks: the exact repeated-addition walker on the host and on the device ----

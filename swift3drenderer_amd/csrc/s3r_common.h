@@ -82,32 +82,40 @@ S3R_HD float regular_steps(float s, float d, float delta, uint32_t e) {
 // Inside one binade every sum s + d rounds onto the grid u, and the step fl(s + d) - s is the same
 // for every s there (for a d exactly half-way between grid points the tie-to-even parity settles
 // after at most one step).  Once two consecutive steps are equal and in the binade, all
-// regular_steps() steps up to the binade edge are s + j*delta (exact), then one ordinary add crosses
-// the edge.  Near zero (|s| < 4|d|, or < 8|d| heading towards zero) we take single steps.
-// Validated against the sequential loop (tests/test_exact_walk.py).
+// regular_steps() steps up to the binade edge are s + j*delta (exact); one ordinary add then
+// crosses the edge -- one loop iteration per binade.  Near zero (|s| < 8|d|, where binades hold
+// too few steps to jump) the walk takes the reference's own single adds in a tight inner loop; a
+// monotone walk passes that zone at most once.  Validated against the sequential loop on host and
+// device (tests/test_exact_walk.py).
 S3R_HD float exact_walk(float s, float d, uint32_t n, uint32_t *iters = nullptr) {
     if (n == 0) return s;
     const float ad = fabsf(d);
     if (ad == 0.0f || !is_finite(s) || !is_finite(d)) return s + d;   // one add is a fixed point
-    const float ad4 = 4.0f * ad, ad8 = 8.0f * ad;
-    // Branch-free body: every iteration computes the single step and the maximal jump and selects,
-    // so the lanes of a wave only diverge at the loop exit.
-    while (n != 0u) {
+    const float ad8 = 8.0f * ad;
+    for (;;) {
+        while ((n != 0u) & (fabsf(s) < ad8)) {   // near zero: single steps
+            if (iters) ++*iters;
+            s = s + d;
+            n--;
+        }
+        if (n == 0u) break;
         if (iters) ++*iters;
-        const float as = fabsf(s);
-        const bool towards_zero = (s < 0.0f) != (d < 0.0f);
+        const uint32_t e = fexp(s);
         const float s1 = s + d;
         const float s2 = s1 + d;
-        const uint32_t e = fexp(s);
         const float delta = s1 - s;           // exact whenever `steady`
         // non-short-circuit '&' keeps hipcc from turning the test into nested branches
-        const bool steady = (as >= ad4) & !(towards_zero & (as < ad8)) & (n >= 2u) & (e >= 32u) & (e < 254u) &
-                            (fexp(s1) == e) & (fexp(s2) == e) & (delta == s2 - s1);
+        const bool steady = (e >= 32u) & (e < 254u) & (fexp(s1) == e) & (fexp(s2) == e) & (delta == s2 - s1);
         if (steady & (delta == 0.0f)) break;  // fl(s + d) == s: stagnated for good
-        float j = fminf(regular_steps(s, d, delta, e), (float)n);
-        const bool jump = steady & (j >= 2.0f);
-        s = jump ? s + j * delta : s1;        // exact: lands on the grid, at most on the edge
-        n -= jump ? (uint32_t)j : 1u;
+        // steady: j regular steps (exact: lands on the grid, at most on the edge), then one add
+        // across the edge; otherwise (a tie-to-even step, a non-finite value) one single add
+        const float j = steady ? fminf(regular_steps(s, d, delta, e), (float)n) : 0.0f;
+        s = steady ? s + j * delta : s;
+        n -= (uint32_t)j;
+        if (n != 0u) {
+            s = s + d;
+            n--;
+        }
     }
     return s;
 }

@@ -35,14 +35,19 @@ def main():
     out = (ctypes.c_uint64 * 16)()
     lib.s3r_stats(out, 1)
     r.update_and_render(a.width, a.height, poses.hold(a.pose))
-    lib.s3r_stats(out, 1)
+    lib.s3r_stats(out, 0)
     segs = (a.width + 1023) // 1024
     waves = a.height * segs
     print(f'{a.scene}/{a.pose} {a.width}x{a.height}: {waves} waves')
     for k, n in enumerate(NAMES):
         print(f'  {n:15s} lane-sum {out[2 * k]:>14d}  per-wave(sum of wave-max) {out[2 * k + 1]:>12d}'
               f'  per wave {out[2 * k + 1] / waves:10.1f}')
-    print(f'  k_rowstart: row-walk iterations sum {out[12]} max/lane {out[13]}; segment walks sum {out[14]} max/lane {out[15]}')
+    print(f'  k_geometry: row-walk iterations sum {out[12]} max/lane {out[13]}; segment walks sum {out[14]} max/lane {out[15]}')
+    lib.s3r_stats_geometry.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    g = (ctypes.c_uint64 * 8)()
+    lib.s3r_stats_geometry(g)
+    print(f'  k_geometry wall clock: max WG setup {g[0] * 10 / 1e3:.2f} us, max WG {g[1] * 10 / 1e3:.2f} us, '
+          f'first start -> last end {(g[3] - g[2]) * 10 / 1e3:.2f} us')
 
 
 if __name__ == '__main__':
