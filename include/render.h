@@ -95,6 +95,9 @@ void s3r_stats(uint64_t out[16], int reset);
 /* Stats build: the geometry kernel's wall-clock profile (100 MHz ticks): {max workgroup setup time,
  * max workgroup time, first start, last end, 0, 0, 0, 0}. */
 void s3r_stats_geometry(uint64_t out[8]);
+/* Timing build (-DS3R_WGTIME): the last fragment launch's per-workgroup phase timestamps (100 MHz wall clock):
+ * out[4 * wg + k], k = 0 start, 1 list loaded, 2 walk state loaded, 3 end; returns workgroups copied. */
+uint32_t s3r_stats_wg_times(uint64_t *out, uint32_t max_wg);
 
 /* Self-test hooks (tests only): out[i] = the float32 value after n[i] sequential steps
  * s = fl(s + d) (the render.cpp:374/:378 walk) computed by the library's O(binades) walker;

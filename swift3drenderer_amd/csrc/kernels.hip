@@ -218,6 +218,7 @@ __device__ void geo_slot_setup(uint32_t s, uint32_t ntri, const float4 *__restri
 #ifdef S3R_STATS
 __device__ unsigned long long g_stats[16];
 __device__ unsigned long long g_tstats[8];   // k_geometry wall-clock (100 MHz) profile, stats build
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
     return v;
@@ -225,6 +226,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #define S3R_IT(p) , (p)
 #else
 #define S3R_IT(p)
+#endif
+
+// Timing build (-DS3R_WGTIME, tools/wg_timeline.py): per-workgroup phase timestamps of k_fragment.
+constexpr uint32_t kWgTimesMax = 65536;
+#ifdef S3R_WGTIME
+__device__ unsigned long long g_wgt[kWgTimesMax * 4];   // wave 0's 100 MHz wall clock per phase
+#define S3R_WGT(k) do { if (threadIdx.x == 0 && blockIdx.x < kWgTimesMax) g_wgt[blockIdx.x * 4 + (k)] = wall_clock64(); } while (0)
+#else
+#define S3R_WGT(k) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------ ripmap sample
@@ -379,6 +389,21 @@ __device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, u
     load_entries(tris, sh, sh.cnt, wave, lane);
 }
 
+// rowtab: exact walk values of a row at x = xmin (j = 0) and at every start-table boundary
+// x = j' * kStartPx inside (xmin, xmax] (j = 1 + j').  The start point of a walk to pixel xs >= xmin:
+// the last tabulated point at or before xs.  Fragment segments narrower than kStartPx walk the
+// remaining < kStartPx pixels themselves (a few exact_walk iterations), so the geometry's serial
+// chain does not grow with the number of fragment segments.
+constexpr uint32_t kStartPx = 384;
+__device__ __forceinline__ uint32_t start_index(uint32_t xmin, uint32_t xs, uint32_t *k) {
+    const uint32_t jb = xs / kStartPx;
+    if (xs <= xmin || jb * kStartPx <= xmin) { *k = xmin; return 0u; }
+    *k = jb * kStartPx;
+    return 1u + jb;
+}
+S3R_HD uint32_t start_entries_of(uint32_t W) { return (W + kStartPx - 1) / kStartPx + 1u; }
+uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
+
 // ------------------------------------------------------------------ K1: geometry, one launch
 // Per frame, on the geometry stream (overlapping the previous frame's fragment kernel): one
 // workgroup per (slot, block of kGeoRows local rows) x 3 components.
@@ -390,8 +415,8 @@ __device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, u
 //   * starts: lane (row, component) walks the reference's sequence exactly (exact_walk): wy += dy
 //     down to its row (render.cpp:378), then w += dx along the row through every fragment-segment
 //     boundary inside the bbox (:374), storing the row start and each segment start.
-// rowtab[((slot * rows_local + lr) * (segs + 1) + j) * 4 + c]: j = 0 at x = xmin, j = 1 + s at
-// x = s * segw (only boundaries in (xmin, xmax] are written).
+// rowtab[((slot * rows_local + lr) * nst + j) * 4 + c], nst = start_entries(W): j = 0 at x = xmin,
+// j = 1 + j' at x = j' * kStartPx (only boundaries in (xmin, xmax] are written).
 constexpr uint32_t kGeoRows = 128;
 static_assert(kGeoRows % kWaves == 0, "geometry row blocks hold whole fragment row blocks");
 
@@ -442,7 +467,11 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
     if (lr >= rows_local) return;
     const uint32_t y = row_of(lr);
     if (y < ymin || y > ymax || y >= H) return;
-    float *row = rowtab + ((size_t)slot * rows_local + lr) * (segs + 1) * 4 + c;
+#if defined(S3R_GEO_ABLATE)                  // 2 = no walks at all
+    if (S3R_GEO_ABLATE & 2) return;
+#endif
+    const uint32_t nst = start_entries_of(W);
+    float *row = rowtab + ((size_t)slot * rows_local + lr) * nst * 4 + c;
     const float d = sts.dx[c];
 #ifdef S3R_STATS
     uint32_t it_row = 0, it_seg = 0;
@@ -451,9 +480,12 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
     float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
 #endif
     row[0] = v;
+#if defined(S3R_GEO_ABLATE)                  // timing-only variants: 1 = no segment starts
+    if (S3R_GEO_ABLATE & 1) return;
+#endif
     uint32_t xp = xmin;
-    for (uint32_t sg = xmin / segw + 1u; sg < segs; sg++) {
-        const uint32_t xb = sg * segw;
+    for (uint32_t sg = xmin / kStartPx + 1u; sg + 1u < nst; sg++) {
+        const uint32_t xb = sg * kStartPx;
         if (xb > xmax) break;
 #ifdef S3R_STATS
         v = exact_walk(v, d, xb - xp, &it_seg);
@@ -474,16 +506,11 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
 #endif
 }
 
-// Deferred shading of the winning triangle (render.cpp:366-371).
-S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
-                                       const uint32_t *__restrict__ tex, uint32_t ntex) {
-    const float4 *q = reinterpret_cast<const float4 *>(tp);
-    const uint4 hdr = reinterpret_cast<const uint4 *>(tp)[0];
-    const uint4 hdr2 = reinterpret_cast<const uint4 *>(tp)[1];
-    const uint32_t kind = hdr.x, tex_base = hdr2.y;
-    const float4 c0 = q[6], c1 = q[7], c2 = q[8];      // cvr
-    const float4 n0 = q[9], n1 = q[10], n2 = q[11];    // nr
-    const float4 k0 = q[12], k1 = q[13], k2 = q[14];   // col
+// Deferred shading of the winning triangle (render.cpp:366-371) from its constants: cvr (c0-c2),
+// nr (n0-n2), col (k0-k2), kind and texture base.
+S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0, float4 k1,
+                               float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1, float w2, float ooz,
+                               const uint32_t *__restrict__ tex, uint32_t ntex) {
     const float a = w0 / ooz, b = w1 / ooz, c = w2 / ooz;
     const F3 P = mk3((c0.x * a + c1.x * b) + c2.x * c, (c0.y * a + c1.y * b) + c2.y * c,
                      (c0.z * a + c1.z * b) + c2.z * c);
@@ -508,6 +535,14 @@ S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, f
         col = mk3((float)(rgb >> 16), (float)((rgb >> 8) & 255u), (float)(rgb & 255u));
     }
     return rgb_pack(s * col.x, s * col.y, s * col.z);
+}
+
+// The same from a TriSetup record (tile path: a register-resident record).
+S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
+                          const uint32_t *__restrict__ tex, uint32_t ntex) {
+    const float4 *q = reinterpret_cast<const float4 *>(tp);
+    return shade_core(q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], tp->kind, tp->tex_base, w0, w1, w2,
+                      ooz, tex, ntex);
 }
 
 // Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle.
@@ -634,8 +669,10 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   uint32_t rows_local, uint32_t *__restrict__ binmask,
                                                   uint32_t nwords) {
     __shared__ FragShared sh;
+    S3R_WGT(0);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t blk = blockIdx.x / segs, seg = blockIdx.x - blk * segs;
+    const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
     const uint32_t lr0 = blk * kWaves;
     const uint32_t lr = lr0 + wave;
@@ -688,31 +725,34 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         load_entries(tris, sh, sh.cnt, wave, lane);
         overflow = false;
     } else {
+        // > kListMax triangles meet this workgroup: stateless rounds of in-kernel slot scans
         build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
-        overflow = sh.next < nslots;           // > kListMax triangles: stateless rounds per chunk
+        overflow = true;
     }
     const uint32_t n0 = sh.cnt;
+    S3R_WGT(1);
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 16)
     if (false) {
 #else
     if (!overflow && row_ok) {
 #endif
-        // walk state of the first batches: the exact row start (rowtab) at x = xmin
+        // walk state of the first batches: the exact value AT each listed triangle's first pixel in
+        // the segment, or at the last start-table point before it
         for (uint32_t b = 0; b < kStateBatches && b * kTPB < n0; b++) {
             const uint32_t idx = b * kTPB + tl;
             if (lane < 63 && idx < n0) {
                 const Entry &e = sh.ent[idx];
                 if (y >= e.ymin && y <= e.ymax) {
-                    // exact value AT this triangle's first pixel in the segment (xmin, or the
-                    // segment start): the first chunk then needs no walking at all
-                    const bool inside = e.xmin >= xs;
-                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * rows_local + lr) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
-                    st_k[b * 64 + lane] = inside ? e.xmin : xs;
+                    uint32_t k;
+                    const uint32_t j = start_index(e.xmin, xs, &k);
+                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
+                    st_k[b * 64 + lane] = k;
                 }
             }
         }
         wave_sync();
     }
+    S3R_WGT(2);
 
     // ---- batch 0 (the first kTPB listed triangles: nearly every row has no more) keeps its
     // constants, walk state and current linear run in registers
@@ -819,9 +859,10 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                             const float cp = st_c[b * 64 + lane];
                             v.c = v.k0 == kp ? cp : (v.k0 == kp + 1u ? cp + v.d : walk(cp, v.d, v.k0 - kp S3R_IT(p_chunk)));
                         } else {
-                            const bool inside = e.xmin >= xs;
-                            const float c0v = rowtab[(((size_t)e.slot * rows_local + lr) * (segs + 1) + (inside ? 0 : 1 + seg)) * 4 + comp];
-                            v.c = walk(c0v, v.d, v.k0 - (inside ? e.xmin : xs) S3R_IT(p_chunk));
+                            uint32_t k;
+                            const uint32_t j = start_index(e.xmin, xs, &k);
+                            const float c0v = rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
+                            v.c = walk(c0v, v.d, v.k0 - k S3R_IT(p_chunk));
                         }
                         v.lin = chunk_linear(v.c, v.d, v.m, &v.del);
                         if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;
@@ -854,6 +895,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
 #endif
         }
     }
+    S3R_WGT(3);
 #ifdef S3R_STATS
     {
         const uint32_t vals[6] = {st_row, st_chunk, st_pix, st_irr, st_tests, st_batches};
@@ -1290,6 +1332,18 @@ void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *
                       uint32_t count, hipStream_t st) {
     if (count == 0) return;
     hipLaunchKernelGGL(k_walk_test, dim3((count + 255) / 256), dim3(256), 0, st, s, d, n, out, lin, del, count);
+}
+
+uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg) {
+#ifdef S3R_WGTIME
+    (void)hipDeviceSynchronize();
+    const uint32_t n = max_wg < kWgTimesMax ? max_wg : kWgTimesMax;
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgt), sizeof(unsigned long long) * 4 * n, 0, hipMemcpyDeviceToHost);
+    return n;
+#else
+    (void)out; (void)max_wg;
+    return 0;
+#endif
 }
 
 void stats_read(unsigned long long out[24], bool reset) {

@@ -452,7 +452,7 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     }
     g.last_path = 1;
     fragment_configure(W, rows_local);
-    const size_t need = (size_t)2 * g.ntri * rows_local * (fragment_segments(W) + 1) * 4;
+    const size_t need = (size_t)2 * g.ntri * rows_local * start_entries(W) * 4;
     if (g.rowtab_cap < need) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
@@ -475,7 +475,8 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     const uint32_t p = next_set();
     hipStream_t geo = g.geo[g.frame_no % kGeoStreams];
     hp.lap(1);
-    HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
+    // the set's last reader (frame k - kSets) has usually finished: then no cross-stream wait
+    if (g.serial || hipEventQuery(g.frag_done[p]) != hipSuccess) HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
     if (g.serial) wait_all_fragments(geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     hp.lap(2);
@@ -617,6 +618,13 @@ __attribute__((visibility("default"))) void s3r_stats(uint64_t out[16], int rese
     unsigned long long tmp[24];
     stats_read(tmp, reset != 0);
     for (int i = 0; i < 16; i++) out[i] = tmp[i];
+}
+
+// Timing build only (-DS3R_WGTIME): the last k_fragment launch's per-workgroup phase timestamps (100 MHz wall clock,
+// wave 0): out[4 * wg + k], k = 0 start, 1 list loaded, 2 walk state loaded, 3 end.  Returns the
+// number of workgroups copied (0 in the product build).
+__attribute__((visibility("default"))) uint32_t s3r_stats_wg_times(uint64_t *out, uint32_t max_wg) {
+    return wg_times_read(reinterpret_cast<unsigned long long *>(out), max_wg);
 }
 
 // Stats build only: k_geometry wall-clock profile (100 MHz ticks): {max setup time of a workgroup,

@@ -18,8 +18,9 @@ uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
 uint32_t bin_words(uint32_t nslots);
 
 // The frame's geometry in one launch (k_geometry): TriSetup records for the 2T slots, the slot
-// masks, and rowtab (2T x rows_local x (segments + 1) x float4): exact barycentrics of every live
-// slot's bbox rows at x = xmin and at each fragment-segment boundary inside the bbox.
+// masks, and rowtab (2T x rows_local x start_entries(W) x float4): exact barycentrics of every live
+// slot's bbox rows at x = xmin and at each 384-pixel boundary inside the bbox.
+uint32_t start_entries(uint32_t W);
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
@@ -52,6 +53,7 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          uint32_t rows_local, hipStream_t st);
 
 void stats_read(unsigned long long out[24], bool reset);
+uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);
 
 void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,
                       uint32_t count, hipStream_t st);
