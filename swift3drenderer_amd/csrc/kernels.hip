@@ -19,6 +19,8 @@
 #include "s3r_common.h"
 #include "s3r_kernels.h"
 
+#include <hip/hip_ext.h>
+
 namespace s3r {
 
 // ------------------------------------------------------------------ transforms
@@ -1372,9 +1374,9 @@ static_assert(kSegChunks * kChunk == S3R_SEG_PIXELS, "segment = whole chunks");
 static_assert(kSegChunks == 6, "k_fragment instantiations below: 6, 3, 2, 1 chunks");
 
 // Segment width of this frame's row path: the widest of 6, 3, 2, 1 chunks that still launches at
-// least kMinFragBlocks workgroups (~20 per CU), so small frames fill the chip (a 1080p frame at
+// least kMinFragBlocks workgroups (~8 per CU), so small frames fill the chip (a 1080p frame at
 // 6 chunks is 1350 workgroups; each runs a latency-bound chain, so too few leave CUs idle).
-constexpr uint64_t kMinFragBlocks = 5000;   // measured: 1080p best at 1 chunk (8100 WGs), 4K at 6 (5400 WGs)
+constexpr uint64_t kMinFragBlocks = 2000;   // measured best or near-best for 4K at 1, 2, 4, 8 row-band parts and 1080p
 static uint32_t g_segch = kSegChunks;
 
 void fragment_configure(uint32_t W, uint32_t rows_local) {
@@ -1399,22 +1401,30 @@ uint32_t bin_words(uint32_t nslots) { return (nslots + 31u) / 32u; }
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st) {
-    if (ntri == 0 || rows_local == 0) return;
-    hipLaunchKernelGGL(k_geometry, dim3(2 * ntri, (rows_local + kGeoRows - 1) / kGeoRows), dim3(3 * kGeoRows), 0, st,
-                       vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band, nparts, part, rows_local,
-                       fragment_segments(W), kChunk * g_segch, bin_words(2 * ntri), tris, rowtab, binmask);
+                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st, hipEvent_t done) {
+    if (ntri == 0 || rows_local == 0) {
+        if (done) (void)hipEventRecord(done, st);
+        return;
+    }
+    // the completion event is recorded by the launch itself (one host call instead of two)
+    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri, (rows_local + kGeoRows - 1) / kGeoRows), dim3(3 * kGeoRows), 0,
+                          st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band, nparts,
+                          part, rows_local, fragment_segments(W), kChunk * g_segch, bin_words(2 * ntri), tris, rowtab,
+                          binmask);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *binmask, hipStream_t st) {
+                     uint32_t rows_local, uint32_t *binmask, hipStream_t st, hipEvent_t done) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
-    if (blocks == 0) return;
+    if (blocks == 0) {
+        if (done) (void)hipEventRecord(done, st);
+        return;
+    }
     auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out, W,
-                       H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots));
+    hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots, rowtab,
+                          tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots));
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

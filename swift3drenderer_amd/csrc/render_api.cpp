@@ -481,17 +481,15 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     hp.lap(2);
     launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], geo);
+                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], geo, g.geo_done[p]);
     hp.lap(3);
-    HIPCHECK(hipEventRecord(g.geo_done[p], geo));
     // fragment on the caller's stream
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.binmask[p], st);
+                    g.binmask[p], st, g.frag_done[p]);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
-    HIPCHECK(hipEventRecord(g.frag_done[p], st));
     HIPCHECK(hipGetLastError());
     hp.lap(5);
     hp.frames++;

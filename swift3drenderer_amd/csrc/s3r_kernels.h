@@ -4,12 +4,13 @@
 
 namespace s3r {
 
+// `done` (may be null): recorded on `st` when the launched kernel completes.
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *binmask, hipStream_t st);
+                     uint32_t rows_local, uint32_t *binmask, hipStream_t st, hipEvent_t done);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their slot masks:
 // fragment_bins() masks of bin_words(nslots) u32 each, all zero between frames (the fragment kernel
@@ -24,7 +25,7 @@ uint32_t start_entries(uint32_t W);
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st);
+                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st, hipEvent_t done);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
