@@ -935,7 +935,8 @@ constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of on
 constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
 
 struct alignas(16) RasterRec {                     // 64 B: one line per live slot
-    uint32_t bx, by, slot, pad;                    // bx = xmin | xmax << 16, by = ymin | ymax << 16
+    uint32_t bx, by, slot, zb;                     // bx = xmin | xmax << 16, by = ymin | ymax << 16,
+                                                   // zb = bits of ooz_bound() (hierarchical depth cull)
     float ws[3], dx0;
     float dx12[2], dy01[2];
     float dy2, rz[3];
@@ -1009,9 +1010,44 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
     }
 }
 
+// A strict upper bound of every 1/z the triangle can produce at a pixel it covers, i.e. of
+// ooz = (r0*a0 + r1*a1) + r2*a2 (render.cpp:363) over walked values a_i >= 0 (:362).  The walked
+// a_i of pixel (x, y) come from <= nx + ny float adds (:374, :378) through values inside the bbox,
+// where the exact affine w*_i(kx, ky) = ws_i + ky*dy_i + kx*dx_i is bounded by its corners: with M
+// the largest |w*_i| at a corner and S the largest corner sum of w*_0 + w*_1 + w*_2, each add rounds
+// by <= 2^-24 (M + 1), so a0 + a1 + a2 <= S + 3 (nx + ny) 2^-24 (M + 1); the three products and two
+// sums add <= 2^-22 relative (r_i = 1/z_i > 0 past the near plane).  Evaluated in double with a
+// further 2^-20 margin and rounded up.  A pixel whose current winner has a larger 1/z cannot be won
+// by this triangle (strict '>' at :364), so k_tile_raster may skip it.
+__device__ float ooz_bound(const TriSetup &t) {
+    const double nx = (double)(t.xmax - t.xmin), ny = (double)(t.ymax - t.ymin);
+    double S = -1e300, M = 0.0;
+#pragma unroll
+    for (int cx = 0; cx < 2; cx++) {
+#pragma unroll
+        for (int cy = 0; cy < 2; cy++) {
+            double sum = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const double w = (double)t.ws[i] + (cy ? ny : 0.0) * (double)t.dy[i] + (cx ? nx : 0.0) * (double)t.dx[i];
+                sum += w;
+                M = fmax(M, fabs(w));
+            }
+            S = fmax(S, sum);
+        }
+    }
+    const double asum = S + 3.0 * (nx + ny + 1.0) * (M + 1.0) * 0x1p-24;
+    const double rmax = fmax(fmax((double)t.rvz[0], (double)t.rvz[1]), (double)t.rvz[2]);
+    const double b = rmax * asum * (1.0 + 0x1p-20) + 0x1p-126;
+    const float f = (float)b;
+    const float up = (double)f >= b ? f : u2f(f2u(f) + 1u);   // round up (b > 0)
+    return is_finite(up) && rmax > 0.0 && asum > 0.0 ? up : __builtin_inff();
+}
+
 __device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot) {
     float4 *q = reinterpret_cast<float4 *>(r);
-    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot, 0u);
+    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot,
+                                                 f2u(ooz_bound(t)));
     q[1] = make_float4(t.ws[0], t.ws[1], t.ws[2], t.dx[0]);
     q[2] = make_float4(t.dx[1], t.dx[2], t.dy[0], t.dy[1]);
     q[3] = make_float4(t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]);
@@ -1117,6 +1153,8 @@ struct TileShared {
     uint32_t pre[kTileStage + 1];
     uint16_t item[kTileStage * kTileH];            // item -> staged triangle
     uint32_t wsum[kTileThreads / 64];
+    uint32_t zmin[kTileH][kTileW / 16];            // per tile row and 16-px group: min over its pixels of
+                                                   // bits(1/z) of the current winner (0: a pixel has none)
 };
 
 // Shading constants of slot s recomputed from the scene exactly as k_setup computes them.
@@ -1173,8 +1211,23 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         }
     };
     fetch(0);
+#ifdef S3R_STATS
+    uint32_t st_staged = 0, st_culled = 0;
+#endif
     for (uint32_t c0 = 0; c0 < n; c0 += kTileStage) {
         __syncthreads();                                 // previous stage fully consumed
+#if !(defined(S3R_TNOHIZ) && S3R_TNOHIZ)
+        // hierarchical depth: each tile row's farthest current winner (0 while a pixel has none)
+        if (c0 > 0) {
+            const uint32_t rr = tid >> 4, cc = (tid & 15u) * 4u;
+            const unsigned long long *kr = ls.key + rr * kKeyStride + cc;
+            uint32_t m = min(min((uint32_t)(kr[0] >> 32), (uint32_t)(kr[1] >> 32)),
+                             min((uint32_t)(kr[2] >> 32), (uint32_t)(kr[3] >> 32)));
+            for (int o = 2; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+            if ((tid & 3u) == 0u) ls.zmin[rr][(tid & 15u) >> 2] = m;
+        }
+        __syncthreads();
+#endif
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
         if (tid < kTileStage && j < n) {
@@ -1185,6 +1238,24 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi);
             const uint32_t a = max(lo, tr0), b = min(hi, tr1);
             nr = (lo <= hi && a <= b) ? b - a + 1u : 0u;
+#if !(defined(S3R_TNOHIZ) && S3R_TNOHIZ)
+            // every pixel of rows [a, b] already holds a 1/z above anything this triangle can
+            // produce (ooz_bound): it wins none of them (strict '>', render.cpp:364)
+#ifdef S3R_STATS
+            st_staged += nr ? 1u : 0u;
+#endif
+            if (nr && c0 > 0) {
+                const uint32_t g0 = (max(bx & 0xFFFFu, lx0) - lx0) >> 4, g1 = (min(bx >> 16, lx1) - lx0) >> 4;
+                const uint32_t zb = f2u(q0.w);
+                bool cull = true;
+                for (uint32_t r = a; r <= b && cull; r++)
+                    for (uint32_t g = g0; g <= g1; g++) cull = cull && zb < ls.zmin[r - tr0][g];
+                if (cull) nr = 0;
+#ifdef S3R_STATS
+                st_culled += cull ? 1u : 0u;
+#endif
+            }
+#endif
             ls.slot[tid] = s; ls.xmin[tid] = bx & 0xFFFFu; ls.xmax[tid] = bx >> 16; ls.ymin[tid] = by & 0xFFFFu;
             ls.r0[tid] = a;
             ls.ws[0][tid] = q1.x; ls.ws[1][tid] = q1.y; ls.ws[2][tid] = q1.z;
@@ -1279,6 +1350,15 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             }
         }
     }
+#ifdef S3R_STATS
+    {
+        uint32_t v[2] = {st_staged, st_culled};
+        for (int k = 0; k < 2; k++) {
+            for (int o = 32; o > 0; o >>= 1) v[k] += (uint32_t)__shfl_xor((int)v[k], o);
+            if (lane == 0) atomicAdd(&g_stats[k], (unsigned long long)v[k]);
+        }
+    }
+#endif
     __syncthreads();
     for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {
         const uint32_t rr = i / kTileW, cc = i % kTileW;
