@@ -106,6 +106,11 @@ void s3r_selftest_walk_host(const float *s, const float *d, const uint32_t *n, f
                             float *del, uint64_t count);
 int s3r_selftest_walk_device(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin,
                              float *del, uint32_t count);
+/* Self-test (tests only): the shading stage's range-checked exact division / sqrt sequences against
+ * the IEEE operators on the device.  mode 0: every sqrt input in [2^-96, 2^127); 1: every 1/s for s in
+ * [2^-48, 2^64); 2: `count` hashed in-range quotients; 3: `count` hashed vector normalisations.
+ * out = {mismatches, first mismatching index or ~0}; returns 0 when the test ran. */
+int s3r_selftest_fastmath_device(uint32_t mode, uint64_t count, uint64_t out[2]);
 
 #ifdef __cplusplus
 }

@@ -233,10 +233,28 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // Timing build (-DS3R_WGTIME, tools/wg_timeline.py): per-workgroup phase timestamps of k_fragment.
 constexpr uint32_t kWgTimesMax = 65536;
 #ifdef S3R_WGTIME
-__device__ unsigned long long g_wgt[kWgTimesMax * 4];   // wave 0's 100 MHz wall clock per phase
-#define S3R_WGT(k) do { if (threadIdx.x == 0 && blockIdx.x < kWgTimesMax) g_wgt[blockIdx.x * 4 + (k)] = wall_clock64(); } while (0)
+// slots 0-3: wave 0's 100 MHz wall clock at start, list loaded, walk state loaded, end; 4-6: wave 0's
+// shader-clock cycles summed over its chunks in batch 0, later batches, shading + stores; 7: list length;
+// 8-10: wave 0's chunks whose batch 0 took the slow (walk + linear_run) path, had a non-linear
+// component, and the live triangles its pixel phases tested
+constexpr uint32_t kWgSlots = 12;
+__device__ unsigned long long g_wgt[kWgTimesMax * kWgSlots];
+#define S3R_WGT(k) do { if (threadIdx.x == 0 && blockIdx.x < kWgTimesMax) g_wgt[blockIdx.x * kWgSlots + (k)] = wall_clock64(); } while (0)
+#define S3R_WGC_DECL unsigned long long wgc_t = 0, wgc[3] = {0, 0, 0}; uint32_t wgn[3] = {0, 0, 0}
+#define S3R_WGN(k, v) (wgn[k] += (v))
+#define S3R_WGC_MARK() (wgc_t = clock64())
+#define S3R_WGC_ADD(k) (wgc[k] += clock64() - wgc_t)
+#define S3R_WGC_STORE(n) do { if (threadIdx.x == 0 && blockIdx.x < kWgTimesMax) { \
+    for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 4 + i_] = wgc[i_]; \
+    g_wgt[blockIdx.x * kWgSlots + 7] = (n); \
+    for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 8 + i_] = wgn[i_]; } } while (0)
 #else
 #define S3R_WGT(k) do { } while (0)
+#define S3R_WGC_DECL do { } while (0)
+#define S3R_WGC_MARK() do { } while (0)
+#define S3R_WGC_ADD(k) do { } while (0)
+#define S3R_WGC_STORE(n) do { } while (0)
+#define S3R_WGN(k, v) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------ ripmap sample
@@ -270,6 +288,9 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #endif
 #ifndef S3R_PX
 #define S3R_PX 1
+#endif
+#ifndef S3R_TWO_PIECE
+#define S3R_TWO_PIECE 1                // batch 0: chunks crossing one binade edge as two linear pieces
 #endif
 constexpr uint32_t kPX = S3R_PX;       // pixels per lane: a chunk is 64 * kPX consecutive pixels of a row
 constexpr uint32_t kChunk = 64u * kPX;
@@ -508,20 +529,39 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
 #endif
 }
 
+#ifndef S3R_FASTDIV
+#define S3R_FASTDIV 1                  // shading: trimmed exact division / sqrt sequences in range
+#endif
+#if S3R_FASTDIV
+#define S3R_NORMALIZE fast_normalize3_dev
+#else
+#define S3R_NORMALIZE fast_normalize3
+#endif
+
 // Deferred shading of the winning triangle (render.cpp:366-371) from its constants: cvr (c0-c2),
 // nr (n0-n2), col (k0-k2), kind and texture base.
 S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0, float4 k1,
                                float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1, float w2, float ooz,
                                const uint32_t *__restrict__ tex, uint32_t ntex) {
-    const float a = w0 / ooz, b = w1 / ooz, c = w2 / ooz;
+    // w / (1/z), three quotients by one divisor: the refined reciprocal is shared (s3r_common.h)
+    float a, b, c;
+#if S3R_FASTDIV
+    if (div_in_range(w0, ooz) & div_in_range(w1, ooz) & div_in_range(w2, ooz)) {
+        const float r = div_recip(ooz);
+        a = div_with_recip(w0, ooz, r); b = div_with_recip(w1, ooz, r); c = div_with_recip(w2, ooz, r);
+    } else
+#endif
+    {
+        a = w0 / ooz; b = w1 / ooz; c = w2 / ooz;
+    }
     const F3 P = mk3((c0.x * a + c1.x * b) + c2.x * c, (c0.y * a + c1.y * b) + c2.y * c,
                      (c0.z * a + c1.z * b) + c2.z * c);
-    const F3 pn = fast_normalize3(P);
+    const F3 pn = S3R_NORMALIZE(P);
     const F3 point = mk3(-pn.x, -pn.y, -pn.z);
     const F3 N = mk3((n0.x * a + n1.x * b) + n2.x * c, (n0.y * a + n1.y * b) + n2.y * c,
                      (n0.z * a + n1.z * b) + n2.z * c);
-    const F3 normal = fast_normalize3(N);
-    const F3 halfway = fast_normalize3(add3(point, normal));
+    const F3 normal = S3R_NORMALIZE(N);
+    const F3 halfway = S3R_NORMALIZE(add3(point, normal));
     const float s = dot3(halfway, normal);
     F3 col;
     if (kind == kColour) {
@@ -531,8 +571,18 @@ S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float
         // uv0=(k0.x,k0.y) uv1=(k0.z,k0.w) uv2=(k1.x,k1.y) dz=(k1.z,k1.w) tpp=(k2.x,k2.y)
         const float mu = (k0.x * a + k0.z * b) + k1.x * c;
         const float mv = (k0.y * a + k0.w * b) + k1.y * c;
-        const float lvx = ooz / fabsf(k2.x - mu * k1.z);
-        const float lvy = ooz / fabsf(k2.y - mv * k1.w);
+        const float dvx = fabsf(k2.x - mu * k1.z), dvy = fabsf(k2.y - mv * k1.w);
+        float lvx, lvy;
+#if S3R_FASTDIV
+        if (div_in_range(ooz, dvx) & div_in_range(ooz, dvy)) {
+            lvx = div_with_recip(ooz, dvx, div_recip(dvx));
+            lvy = div_with_recip(ooz, dvy, div_recip(dvy));
+        } else
+#endif
+        {
+            lvx = ooz / dvx;
+            lvy = ooz / dvy;
+        }
         const uint32_t rgb = texel(tex, ntex, tex_base, mu, mv, lvx, lvy);
         col = mk3((float)(rgb >> 16), (float)((rgb >> 8) & 255u), (float)(rgb & 255u));
     }
@@ -548,13 +598,15 @@ S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, f
 }
 
 // Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle.
+// Batch 0 also knows two-piece chunks (two = true): pixels k <= kb are c + k*del, pixels k > kb are
+// c2 + (k - kb - 1)*del2 (a binade edge crossed inside the chunk).
 struct BatchLanes {
-    bool ov = false, lin = false, neg = false;
-    float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f;
-    uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
+    bool ov = false, lin = false, neg = false, two = false;
+    float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f, c2 = 0.0f, del2 = 0.0f;
+    uint32_t k0 = 0, m = 0, xmax = 0, slot = 0, kb = 0;
 };
 struct BatchMasks {
-    uint64_t ovm, negm, irrm;
+    uint64_t ovm, negm, irrm, twom;
     uint32_t tix;
 };
 
@@ -570,11 +622,12 @@ __device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32
 ) {
     bm.ovm = __ballot(v.ov && (lane - 3u * tl) == 0u);
     bm.tix = kNoTable;
-    last = v.c + (float)(v.m - 1u) * v.del;
-    if (bm.ovm == 0) { bm.negm = bm.irrm = 0; return; }
+    last = v.two ? v.c2 + (float)(v.m - 2u - v.kb) * v.del2 : v.c + (float)(v.m - 1u) * v.del;
+    if (bm.ovm == 0) { bm.negm = bm.irrm = bm.twom = 0; return; }
     bm.negm = __ballot(v.neg);
-    bm.irrm = __ballot(v.ov && !v.lin && !((bm.negm >> (3u * tl)) & 7ull));
-    if (v.ov && !v.lin) {
+    bm.twom = __ballot(v.ov && v.two);
+    bm.irrm = __ballot(v.ov && !v.lin && !v.two && !((bm.negm >> (3u * tl)) & 7ull));
+    if (v.ov && !v.lin && !v.two) {
         if ((bm.negm >> (3u * tl)) & 7ull) {
             last = v.c;                       // pruned: keep the state at the chunk start
             v.m = 1u;
@@ -613,7 +666,7 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
         live &= live - 1;
         const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0);
         float cv[3], dv[3], r[3];
-        uint32_t lmask = 0;
+        uint32_t lmask = 0, tmask = 0;
 #pragma unroll
         for (uint32_t cc = 0; cc < 3; cc++) {
             const uint32_t l = l0 + cc;
@@ -621,6 +674,7 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
             dv[cc] = rdl(v.del, l);
             r[cc] = rdl(v.rz, l);
             lmask |= (uint32_t)((bm.irrm >> l) & 1ull) << cc;
+            tmask |= (uint32_t)((bm.twom >> l) & 1ull) << cc;
         }
         const int tslot = (int)rdl(v.slot, l0);
 #pragma unroll
@@ -638,7 +692,10 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
                 a[cc] = cv[cc] + fo * dv[cc];
 #else
-                if (!((lmask >> cc) & 1u)) {
+                if ((tmask >> cc) & 1u) {
+                    const uint32_t l = l0 + cc, kb = rdl(v.kb, l);           // two linear pieces
+                    a[cc] = off <= kb ? cv[cc] + fo * dv[cc] : rdl(v.c2, l) + (float)(off - kb - 1u) * rdl(v.del2, l);
+                } else if (!((lmask >> cc) & 1u)) {
                     a[cc] = cv[cc] + fo * dv[cc];                      // linear chunk (or pruned: unused)
                 } else {
                     const uint32_t l = l0 + cc;
@@ -775,6 +832,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     }
 
     uint32_t *row = out + (size_t)lr * W;
+    S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + kChunk * q;
         if (cx0 > xe) break;
@@ -785,6 +843,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
 #pragma unroll
         for (uint32_t p = 0; p < kPX; p++) { depth[p] = 0.0f; bw0[p] = bw1[p] = bw2[p] = 0.0f; win[p] = -1; }
 
+        S3R_WGC_MARK();
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 8)
         if (false) {
 #else
@@ -803,24 +862,52 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                     v.del = r0_del;
                     v.lin = true;
                 } else {
-                    // state = exact value at pixel r0_sk: contiguous chunks need 0 or 1 step
-                    v.c = v.k0 == r0_sk ? r0_sc
-                                        : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
-                    const float j = linear_run(v.c, v.d, &v.del);
-                    v.lin = j >= (float)(v.m - 1u);
-                    if (j >= 1.0f) {
-                        r0_base = v.c; r0_k = v.k0; r0_del = v.del;
-                        r0_end = j >= 65536.0f ? 0xFFFFFFFFu : v.k0 + (uint32_t)j;
+                    S3R_WGN(0, 1u);
+                    float j;
+                    if (v.k0 >= r0_k && v.k0 <= r0_end) {
+                        // the current run ends inside this chunk: its remaining j regular steps
+                        v.c = r0_base + (float)(v.k0 - r0_k) * r0_del;
+                        v.del = r0_del;
+                        j = (float)(r0_end - v.k0);
                     } else {
-                        r0_k = 1u; r0_end = 0u;
+                        // state = exact value at pixel r0_sk: contiguous chunks need 0 or 1 step
+                        v.c = v.k0 == r0_sk ? r0_sc
+                                            : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
+                        j = linear_run(v.c, v.d, &v.del);
+                        if (j >= 1.0f) {
+                            r0_base = v.c; r0_k = v.k0; r0_del = v.del;
+                            r0_end = j >= 65536.0f ? 0xFFFFFFFFu : v.k0 + (uint32_t)j;
+                        } else {
+                            r0_k = 1u; r0_end = 0u;
+                        }
                     }
+                    v.lin = j >= (float)(v.m - 1u);
+#if S3R_TWO_PIECE
+                    if (!v.lin) {
+                        // a binade edge inside the chunk: pixels 0..j are c + k*delta (exact), pixel
+                        // j + 1 is the reference's one add across the edge, and from there the next
+                        // binade's run -- two linear pieces when that run reaches the chunk end
+                        const uint32_t ji = (uint32_t)j;
+                        const float c2 = (v.c + (float)ji * v.del) + v.d;            // render.cpp:374
+                        float d2;
+                        const float j2 = linear_run(c2, v.d, &d2);
+                        if (j2 >= (float)(v.m - 2u - ji)) {
+                            v.two = true; v.c2 = c2; v.del2 = d2; v.kb = ji;
+                            r0_base = c2; r0_k = v.k0 + ji + 1u; r0_del = d2;
+                            r0_end = j2 >= 65536.0f ? 0xFFFFFFFFu : r0_k + (uint32_t)j2;
+                        }
+                    }
+#endif
                 }
                 if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;   // monotone walk
+                else if (v.two) v.neg = v.c < 0.0f && v.c2 + (float)(v.m - 2u - v.kb) * v.del2 < 0.0f;
             }
             BatchMasks bm;
             float last;
             batch_resolve(v, tl, lane, sh.tab[wave], bm, last S3R_IT(p_chunk));
             if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
+            S3R_WGN(1, bm.irrm ? 1u : 0u);
+            S3R_WGN(2, (uint32_t)__builtin_popcountll(bm.ovm & ~(bm.negm | (bm.negm >> 1) | (bm.negm >> 2)) & 0x9249249249249249ull));
             if (bm.ovm) {
 #ifdef S3R_STATS
                 st_batches++;
@@ -834,6 +921,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
             }
         }
 
+        S3R_WGC_ADD(0);
+        S3R_WGC_MARK();
         uint32_t cursor = 0, cnt = n0;
         for (;;) {
             if (overflow) {
@@ -883,6 +972,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
             }
             if (!overflow || cursor >= nslots) break;
         }
+        S3R_WGC_ADD(1);
+        S3R_WGC_MARK();
 #pragma unroll
         for (uint32_t p = 0; p < kPX; p++) {
             const uint32_t xp = x + 64u * p;
@@ -896,8 +987,10 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #endif
         }
+        S3R_WGC_ADD(2);
     }
     S3R_WGT(3);
+    S3R_WGC_STORE(n0);
 #ifdef S3R_STATS
     {
         const uint32_t vals[6] = {st_row, st_chunk, st_pix, st_irr, st_tests, st_batches};
@@ -1416,11 +1509,76 @@ void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *
     hipLaunchKernelGGL(k_walk_test, dim3((count + 255) / 256), dim3(256), 0, st, s, d, n, out, lin, del, count);
 }
 
+// Self-test of the trimmed division / sqrt sequences (s3r_common.h) against the compiler's IEEE
+// operators: mode 0 every x in [2^-96, 2^127) for sqrt, mode 1 every s in [2^-48, 2^64) for 1/s (the
+// normalize reciprocal), mode 2 `count` hashed quotient pairs inside div_in_range (all-zero and
+// all-one significands included), mode 3 `count` hashed vectors for the whole normalize.
+// res[0] += mismatches, res[1] = min mismatching index (res[1] initialised to ~0 by the caller).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float hashed_float(uint64_t h, uint32_t e) {
+    uint32_t m = (uint32_t)h & 0x7FFFFFu;
+    const uint32_t sel = (uint32_t)(h >> 40) & 15u;
+    if (sel == 0u) m = 0u;
+    if (sel == 1u) m = 0x7FFFFFu;
+    return u2f(((uint32_t)(h >> 63) << 31) | (e << 23) | m);
+}
+__global__ void __launch_bounds__(256) k_fastmath_test(uint32_t mode, uint64_t count, unsigned long long *res) {
+#if S3R_FASTDIV
+    uint64_t bad = 0, first = ~0ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool ok = true;
+        if (mode == 0u) {
+            const float x = u2f(0x0F800000u + (uint32_t)i);
+            ok = f2u(sqrt_in_range(x)) == f2u(sqrtf(x));
+        } else if (mode == 1u) {
+            const float x = u2f((79u << 23) + (uint32_t)i);
+            ok = f2u(div_with_recip(1.0f, x, div_recip(x))) == f2u(1.0f / x);
+        } else if (mode == 2u) {
+            const uint64_t h1 = mix64(2 * i + 1), h2 = mix64(2 * i + 2);
+            const uint32_t ea = 32u + (uint32_t)(h1 % 191u);
+            const int eb0 = (int)ea + (int)(h2 % 129u) - 64;
+            const uint32_t eb = (uint32_t)min(max(eb0, 32), 222);
+            const float a = hashed_float(h1, ea), b = hashed_float(h2, eb);
+            if (div_in_range(a, b)) ok = f2u(div_with_recip(a, b, div_recip(b))) == f2u(a / b);
+        } else {
+            const uint64_t h1 = mix64(3 * i + 1), h2 = mix64(3 * i + 2), h3 = mix64(3 * i + 3);
+            const uint32_t e0 = 60u + (uint32_t)(h1 % 130u);
+            const F3 v = mk3(hashed_float(h1, e0), hashed_float(h2, e0 - (uint32_t)(h2 % 30u)),
+                             hashed_float(h3, e0 - (uint32_t)(h3 % 30u)));
+            const F3 p = fast_normalize3_dev(v), q = fast_normalize3(v);
+            ok = f2u(p.x) == f2u(q.x) && f2u(p.y) == f2u(q.y) && f2u(p.z) == f2u(q.z);
+        }
+        if (!ok) { bad++; first = min(first, i); }
+    }
+    if (bad) { atomicAdd(&res[0], (unsigned long long)bad); atomicMin(&res[1], (unsigned long long)first); }
+#else
+    (void)mode; (void)count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&res[0], 1ull);   // not built: report failure
+#endif
+}
+
+int fastmath_test(uint32_t mode, uint64_t count, uint64_t out[2]) {
+    if (mode == 0u) count = 0x7F000000ull - 0x0F800000ull;
+    if (mode == 1u) count = (uint64_t)(191u - 79u) << 23;
+    unsigned long long *res = nullptr;
+    if (hipMalloc((void **)&res, 16) != hipSuccess) return -1;
+    const unsigned long long init[2] = {0ull, ~0ull};
+    (void)hipMemcpy(res, init, 16, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_fastmath_test, dim3(8192), dim3(256), 0, nullptr, mode, count, res);
+    const hipError_t e = hipMemcpy(out, res, 16, hipMemcpyDeviceToHost);
+    (void)hipFree(res);
+    return e == hipSuccess ? 0 : -1;
+}
+
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg) {
 #ifdef S3R_WGTIME
     (void)hipDeviceSynchronize();
     const uint32_t n = max_wg < kWgTimesMax ? max_wg : kWgTimesMax;
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgt), sizeof(unsigned long long) * 4 * n, 0, hipMemcpyDeviceToHost);
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wgt), sizeof(unsigned long long) * kWgSlots * n, 0, hipMemcpyDeviceToHost);
     return n;
 #else
     (void)out; (void)max_wg;

@@ -643,6 +643,11 @@ __attribute__((visibility("default"))) void s3r_selftest_walk_host(const float *
     }
 }
 
+__attribute__((visibility("default"))) int s3r_selftest_fastmath_device(uint32_t mode, uint64_t count,
+                                                                       uint64_t out[2]) {
+    return fastmath_test(mode, count, out);
+}
+
 __attribute__((visibility("default"))) int s3r_selftest_walk_device(const float *s, const float *d, const uint32_t *n,
                                                                    float *out, uint32_t *lin, float *del,
                                                                    uint32_t count) {

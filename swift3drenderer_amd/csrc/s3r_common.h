@@ -177,6 +177,65 @@ S3R_HD F3 muls3(F3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 S3R_HD float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }   // simd_dot
 S3R_HD F3 fast_normalize3(F3 a) { return muls3(a, 1.0f / sqrtf(dot3(a, a))); }  // simd_fast_normalize
 
+// ---- correctly rounded division and sqrt without the range-scaling steps (device) ----
+// hipcc expands IEEE a / b on gfx950 as v_div_scale (x2), v_rcp, one Newton step for 1/b, q = a*r,
+// two fma residual corrections, v_div_fmas, v_div_fixup; and sqrtf(x) as a range scale, v_sqrt, the
+// +-1 ulp candidates tested by fma residuals, an unscale and a special-value select.  Inside the
+// ranges below every scaling step is the identity (v_div_scale returns its operand with VCC = 0,
+// v_div_fmas is a plain fma, v_div_fixup passes a finite normal quotient through; x >= 2^-96 skips the
+// sqrt scale), so the trimmed sequences return the same bits as the full ones: correctly rounded.
+// Callers test the range and take the ordinary operator outside it.  Checked exhaustively (sqrt,
+// reciprocal) and on random pairs (quotients) against the compiler's operators on the device
+// (tests/test_exact_walk.py::test_fast_div_sqrt_device).  (The host compilation pass sees plain
+// operators in place of the gfx950 builtins; these are never run on the host.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define S3R_RCP(x) __builtin_amdgcn_rcpf(x)
+#define S3R_SQRT(x) __builtin_amdgcn_sqrtf(x)
+#else
+#define S3R_RCP(x) (1.0f / (x))
+#define S3R_SQRT(x) sqrtf(x)
+#endif
+// biased exponents of a and b in [32, 222], |ea - eb| <= 64: no scaling anywhere (a = +-0 is out of
+// range: the residual corrections would lose the sign of a -0 quotient)
+__device__ __forceinline__ bool div_in_range(float a, float b) {
+    const int ea = (int)fexp(a), eb = (int)fexp(b);
+    return ((unsigned)(ea - 32) <= 190u) & ((unsigned)(eb - 32) <= 190u) & ((unsigned)(ea - eb + 64) <= 128u);
+}
+// refined reciprocal of the v_rcp + Newton step (the r the division sequence uses)
+__device__ __forceinline__ float div_recip(float b) {
+    const float r = S3R_RCP(b);
+    const float e = __builtin_fmaf(-b, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+// a / b from the refined reciprocal r of b (div_in_range(a, b))
+__device__ __forceinline__ float div_with_recip(float a, float b, float r) {
+    const float q0 = a * r;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), r, q0);
+    return __builtin_fmaf(__builtin_fmaf(-b, q1, a), r, q1);
+}
+// sqrtf(x) for x in [2^-96, 2^127): the v_sqrt result corrected by its fma residuals
+__device__ __forceinline__ float sqrt_in_range(float x) {
+    const float s = S3R_SQRT(x);
+    const float sm = u2f(f2u(s) - 1u), sp = u2f(f2u(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    const float t = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : t;
+}
+__device__ __forceinline__ bool sqrt_in_range_ok(float x) { return x >= 0x1p-96f && x < 0x1p127f; }
+
+// simd_fast_normalize(a) = a * (1 / sqrtf(dot(a, a))), exactly, with the trimmed sequences
+__device__ __forceinline__ F3 fast_normalize3_dev(F3 a) {
+    const float d = dot3(a, a);
+    float inv;
+    if (sqrt_in_range_ok(d)) {                   // sqrt in [2^-48, 2^63.5): 1/s in range as well
+        const float s = sqrt_in_range(d);
+        inv = div_with_recip(1.0f, s, div_recip(s));
+    } else {
+        inv = 1.0f / sqrtf(d);
+    }
+    return mk3(a.x * inv, a.y * inv, a.z * inv);
+}
+
 // (uint8_t)(float) as x86 computes it: cvttss2si to int32 (0x80000000 when out of range or NaN),
 // then the low byte (render.cpp:8 RGB macro).
 S3R_HD uint32_t u8_of_float(float f) {

@@ -56,6 +56,7 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);
 
+int fastmath_test(uint32_t mode, uint64_t count, uint64_t out[2]);
 void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,
                       uint32_t count, hipStream_t st);
 

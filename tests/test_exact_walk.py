@@ -168,3 +168,22 @@ def test_device_walk_exact(seed):
     _, lin, _ = run_device(s, d, m)
     truth, _ = linear_truth(s, d, m)
     assert not np.any(lin.astype(bool) & ~truth)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode,count', [(0, 0), (1, 0), (2, 1 << 30), (3, 1 << 26)])
+def test_fast_div_sqrt_device(mode, count):
+    """The shading stage's trimmed exact sequences (s3r_common.h: div_recip / div_with_recip /
+    sqrt_in_range, used only inside their range checks) return the IEEE operators' bits: sqrt over
+    every input of its range, 1/s over every divisor the normalisation can see, and 2^30 hashed
+    in-range quotients (plus 2^26 whole normalisations)."""
+    from conftest import gpu_available
+    if not gpu_available():
+        pytest.skip('no GPU')
+    import torch
+    torch.cuda.init()
+    lib = load_library()
+    lib.s3r_selftest_fastmath_device.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 2)()
+    assert lib.s3r_selftest_fastmath_device(mode, count, out) == 0
+    assert out[0] == 0, f'mode {mode}: {out[0]} mismatches, first at index {out[1]}'

@@ -12,7 +12,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-VARIANTS = {
+import json
+
+# S3R_VARIANTS='{"tag": {"MACRO": value, ...}, ...}' overrides the default set
+VARIANTS = json.loads(os.environ['S3R_VARIANTS']) if os.environ.get('S3R_VARIANTS') else {
     'base': {},
     'st64': {'S3R_TSTAGE': 64},
     'st256': {'S3R_TSTAGE': 256},
@@ -30,7 +33,7 @@ def run():
     out_root = os.path.join(ROOT, 'gpurun_out', 'variants')
     for tag in VARIANTS:
         env = dict(os.environ, S3R_LIB=os.path.join(ROOT, 'build', f'librender_{tag}.so'), TMPDIR='/tmp',
-                   S3R_SERIAL='1')
+                   S3R_SERIAL=os.environ.get('S3R_SERIAL', '1'))
         d = os.path.join(out_root, tag)
         cmd = ['rocprofv3', '--kernel-trace', '--stats', '-d', d, '-o', 'run', '--output-format', 'csv', '--',
                sys.executable, 'bench.py', '--steps', '10', '--warmup', '2', '--no-cpu-baseline', '--no-e2e'] + extra
@@ -41,8 +44,9 @@ def run():
         parts = []
         if stats:
             for row in csv.DictReader(open(stats[0])):
-                if row['Name'].startswith('s3r::'):
-                    parts.append(f"{row['Name'][5:].split('(')[0]} {float(row['AverageNs']) / 1e3:.1f}")
+                if 's3r::' in row['Name']:
+                    name = row['Name'].split('s3r::', 1)[1].split('(')[0]
+                    parts.append(f"{name} {float(row['AverageNs']) / 1e3:.1f}")
         print(f'{tag:8s} fps {fps:>10s}  ' + '  '.join(parts), flush=True)
 
 

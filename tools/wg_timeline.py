@@ -48,9 +48,9 @@ def main():
     for _ in range(20):
         r.render_bands(poses.hold(a.pose), W, H, B, N, 0, buf.data_ptr(), st)
     torch.cuda.synchronize()
-    out = (ctypes.c_uint64 * (4 * 65536))()
+    out = (ctypes.c_uint64 * (12 * 65536))()
     n = lib.s3r_stats_wg_times(out, 65536)
-    t = np.frombuffer(out, dtype=np.uint64)[: 4 * n].reshape(n, 4).astype(np.int64)
+    t = np.frombuffer(out, dtype=np.uint64)[: 12 * n].reshape(n, 12).astype(np.int64)
     t = t[t[:, 3] > 0]
     t0 = t[:, 0].min()
     rel = (t - t0) * 0.01          # us
@@ -60,6 +60,16 @@ def main():
                     ('chunks', rel[:, 3] - rel[:, 2]), ('total', rel[:, 3] - rel[:, 0]), ('start', rel[:, 0])]:
         p = np.percentile(v, [10, 50, 90, 99])
         print(f'  {name:7s} p10 {p[0]:7.2f}  p50 {p[1]:7.2f}  p90 {p[2]:7.2f}  p99 {p[3]:7.2f}  mean {v.mean():7.2f} us')
+    # wave 0's chunk-loop phases (shader clock, summed over the workgroup's chunks) by list length
+    cyc = t[:, 4:7].astype(np.float64)
+    tot = rel[:, 3] - rel[:, 0]
+    heavy = tot >= np.percentile(tot, 90)
+    for lab, m in [('all', np.ones(len(t), bool)), ('slowest 10%', heavy)]:
+        c = cyc[m].mean(axis=0)
+        print(f'  wave-0 cycles ({lab}): batch0 {c[0]:.0f}  later batches {c[1]:.0f}  shade+store {c[2]:.0f}; '
+              f'list length mean {t[m, 7].mean():.1f} max {t[m, 7].max()}')
+        print(f'      per workgroup (wave 0): slow-path chunks {t[m, 8].mean():.2f}, non-linear chunks {t[m, 9].mean():.2f}, '
+              f'live triangles tested {t[m, 10].mean():.2f}')
     edges = np.linspace(0, span, 11)
     live = [int(((rel[:, 0] <= e) & (rel[:, 3] > e)).sum()) for e in edges[:-1]]
     print('  in flight at 0%,10%..90% of the span:', live)
