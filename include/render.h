@@ -98,6 +98,9 @@ void s3r_stats_geometry(uint64_t out[8]);
 /* Timing build (-DS3R_WGTIME): the last fragment launch's per-workgroup phase timestamps (100 MHz wall clock):
  * out[4 * wg + k], k = 0 start, 1 list loaded, 2 walk state loaded, 3 end; returns workgroups copied. */
 uint32_t s3r_stats_wg_times(uint64_t *out, uint32_t max_wg);
+/* Timing build: per geometry workgroup (slot + row block * 2T) of the launches since the last call, 100 MHz
+ * wall clock: out[4 * wg + k], k = 0 start, 1 slot set up, 2 bins set, 3 end; clears them; returns the count. */
+uint32_t s3r_stats_geo_times(uint64_t *out, uint32_t max_wg);
 
 /* Self-test hooks (tests only): out[i] = the float32 value after n[i] sequential steps
  * s = fl(s + d) (the render.cpp:374/:378 walk) computed by the library's O(binades) walker;

@@ -248,7 +248,16 @@ __device__ unsigned long long g_wgt[kWgTimesMax * kWgSlots];
     for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 4 + i_] = wgc[i_]; \
     g_wgt[blockIdx.x * kWgSlots + 7] = (n); \
     for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 8 + i_] = wgn[i_]; } } while (0)
+// k_geometry workgroups (slot + row block * grid x): 0 start, 1 slot set up, 2 bins set, 3 last wave done
+constexpr uint32_t kGeoTimesMax = 8192;
+__device__ unsigned long long g_gwt[kGeoTimesMax * 4];
+#define S3R_GWT(k) do { const uint32_t g_ = blockIdx.x + blockIdx.y * gridDim.x; \
+    if (threadIdx.x == 0 && g_ < kGeoTimesMax) g_gwt[g_ * 4 + (k)] = wall_clock64(); } while (0)
+#define S3R_GWT_END() do { const uint32_t g_ = blockIdx.x + blockIdx.y * gridDim.x; \
+    if ((threadIdx.x & 63u) == 0 && g_ < kGeoTimesMax) atomicMax(&g_gwt[g_ * 4 + 3], wall_clock64()); } while (0)
 #else
+#define S3R_GWT(k) do { } while (0)
+#define S3R_GWT_END() do { } while (0)
 #define S3R_WGT(k) do { } while (0)
 #define S3R_WGC_DECL do { } while (0)
 #define S3R_WGC_MARK() do { } while (0)
@@ -448,13 +457,14 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
     const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, uint32_t nwords, TriSetup *__restrict__ tris,
-    float *__restrict__ rowtab, uint32_t *__restrict__ binmask) {
+    float *__restrict__ rowtab, unsigned long long *__restrict__ binmask, uint32_t tag) {
     __shared__ TriSetup sts;
     const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
 #ifdef S3R_STATS
     const unsigned long long t_start = wall_clock64();
     if (tid == 0) atomicMin(&g_tstats[2], t_start);
 #endif
+    S3R_GWT(0);
     if (tid == 0) {
         TriSetup t;
         geo_slot_setup(slot, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, (float)W, (float)H, t);
@@ -465,7 +475,8 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
 #endif
     }
     __syncthreads();
-    if (sts.kind == kDead) return;
+    S3R_GWT(1);
+    if (sts.kind == kDead) { S3R_GWT_END(); return; }
     const uint32_t xmin = sts.xmin, xmax = sts.xmax, ymin = sts.ymin, ymax = sts.ymax;
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
 
@@ -482,14 +493,25 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
         }
         const uint32_t x0 = sg * segw, x1 = min(W, x0 + segw) - 1u;
         if (ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)
-            atomicOr(&binmask[((size_t)blk * segs + sg) * nwords + (slot >> 5)], 1u << (slot & 31u));
+        {
+            // tagged word (tag << 32 | bits): a word still carrying an older frame's tag starts empty
+            unsigned long long *w = &binmask[((size_t)blk * segs + sg) * nwords + (slot >> 5)];
+            const unsigned long long tagged = (unsigned long long)tag << 32, bit = 1ull << (slot & 31u);
+            unsigned long long old = *w;
+            for (;;) {
+                const unsigned long long nw = (((old >> 32) == tag) ? old : tagged) | bit;
+                const unsigned long long prev = atomicCAS(w, old, nw);
+                if (prev == old) break;
+                old = prev;
+            }
+        }
     }
 
+    S3R_GWT(2);
     // exact row and segment starts
     const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
-    if (lr >= rows_local) return;
     const uint32_t y = row_of(lr);
-    if (y < ymin || y > ymax || y >= H) return;
+    if (lr >= rows_local || y < ymin || y > ymax || y >= H) { S3R_GWT_END(); return; }
 #if defined(S3R_GEO_ABLATE)                  // 2 = no walks at all
     if (S3R_GEO_ABLATE & 2) return;
 #endif
@@ -527,6 +549,7 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
     atomicAdd(&g_stats[14], (unsigned long long)it_seg);
     atomicMax(&g_stats[15], (unsigned long long)it_seg);
 #endif
+    S3R_GWT_END();
 }
 
 #ifndef S3R_FASTDIV
@@ -725,12 +748,20 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
-                                                  uint32_t rows_local, uint32_t *__restrict__ binmask,
-                                                  uint32_t nwords) {
+                                                  uint32_t rows_local,
+                                                  const unsigned long long *__restrict__ binmask,
+                                                  uint32_t nwords, uint32_t done_tag, uint32_t *done_flag,
+                                                  uint32_t prev_tag) {
     __shared__ FragShared sh;
     S3R_WGT(0);
+    // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
+    // launch runs only once the previous fragment launch on its stream has completed, so its first
+    // workgroup publishes that launch's tag in host-coherent memory.
+    if (done_flag && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(done_flag, prev_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t blk = blockIdx.x / segs, seg = blockIdx.x - blk * segs;
+    const uint32_t bid = blockIdx.x;
+    const uint32_t blk = bid / segs, seg = bid - blk * segs;
     const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
     const uint32_t lr0 = blk * kWaves;
@@ -756,12 +787,12 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     // or, beyond kListMax triangles, the first round of an in-kernel slot scan
     bool overflow;
     if (wave == 0) {
-        uint32_t *mw = binmask + (size_t)blockIdx.x * nwords;
+        const unsigned long long *mw = binmask + (size_t)bid * nwords;
         uint32_t cnt = 0;
         for (uint32_t base = 0; base < nwords; base += 64u) {
             const uint32_t i = base + lane;
-            uint32_t w = i < nwords ? mw[i] : 0u;
-            if (w) mw[i] = 0u;                                   // cleared for the buffer's next frame
+            const unsigned long long tw = i < nwords ? mw[i] : 0ull;
+            uint32_t w = (uint32_t)(tw >> 32) == done_tag ? (uint32_t)tw : 0u;   // this frame's bits only
             const uint32_t pc = (uint32_t)__builtin_popcount(w);
             uint32_t inc = pc;
             for (uint32_t o = 1; o < 64u; o <<= 1) {
@@ -1001,6 +1032,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         }
     }
 #endif
+
 }
 
 // ------------------------------------------------------------------ tile path (many triangles)
@@ -1574,6 +1606,21 @@ int fastmath_test(uint32_t mode, uint64_t count, uint64_t out[2]) {
     return e == hipSuccess ? 0 : -1;
 }
 
+uint32_t geo_times_read(unsigned long long *out, uint32_t max_wg) {
+#ifdef S3R_WGTIME
+    (void)hipDeviceSynchronize();
+    const uint32_t n = max_wg < kGeoTimesMax ? max_wg : kGeoTimesMax;
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gwt), sizeof(unsigned long long) * 4 * n, 0, hipMemcpyDeviceToHost);
+    unsigned long long *z = (unsigned long long *)calloc(4 * n, sizeof(unsigned long long));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gwt), z, sizeof(unsigned long long) * 4 * n, 0, hipMemcpyHostToDevice);
+    free(z);
+    return n;
+#else
+    (void)out; (void)max_wg;
+    return 0;
+#endif
+}
+
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg) {
 #ifdef S3R_WGTIME
     (void)hipDeviceSynchronize();
@@ -1639,7 +1686,8 @@ uint32_t bin_words(uint32_t nslots) { return (nslots + 31u) / 32u; }
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st, hipEvent_t done) {
+                     TriSetup *tris, float *rowtab, unsigned long long *binmask, uint32_t tag, hipStream_t st,
+                     hipEvent_t done) {
     if (ntri == 0 || rows_local == 0) {
         if (done) (void)hipEventRecord(done, st);
         return;
@@ -1648,21 +1696,28 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri, (rows_local + kGeoRows - 1) / kGeoRows), dim3(3 * kGeoRows), 0,
                           st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band, nparts,
                           part, rows_local, fragment_segments(W), kChunk * g_segch, bin_words(2 * ntri), tris, rowtab,
-                          binmask);
+                          binmask, tag);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *binmask, hipStream_t st, hipEvent_t done) {
+                     uint32_t rows_local, const unsigned long long *binmask, uint32_t tag, hipStream_t st,
+                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
-    if (blocks == 0) {
+    if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
         if (done) (void)hipEventRecord(done, st);
         return;
     }
     auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
-    hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots, rowtab,
-                          tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots));
+    if (done)
+        hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
+                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binmask,
+                              bin_words(nslots), tag, done_flag, prev_tag);
+    else
+        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
+                           W, H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots), tag, done_flag,
+                           prev_tag);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

@@ -40,7 +40,7 @@ struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
 // Per-frame buffer sets in flight: frame k's geometry writes set k % kSets once the fragment kernel
 // of frame k - kSets (the set's last reader) is done, on geometry stream k % kGeoStreams, so the
 // geometry of two consecutive frames and the previous frame's fragment kernel can all overlap.
-constexpr int kSets = 3;
+constexpr int kSets = 4;
 constexpr int kGeoStreams = 2;
 
 struct Lib {
@@ -67,7 +67,7 @@ struct Lib {
     TriSetup *tris[kSets] = {};
     float *rowtab[kSets] = {};     // 2T x rows x (segments + 1) x float4 exact row starts
     size_t rowtab_cap = 0;
-    uint32_t *binmask[kSets] = {}; // per fragment workgroup: slot mask (zero between frames)
+    unsigned long long *binmask[kSets] = {}; // per fragment workgroup: tagged slot-mask words
     uint64_t binmask_cap = 0;
     // tile path (many triangles): per-tile counts, offsets, scatter cursors, slot lists
     uint32_t *tile_counts[kSets] = {}, *tile_offs[kSets] = {};
@@ -85,6 +85,15 @@ struct Lib {
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
+    // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
+    // fragment launch on its stream (complete by stream order) in *done_host (host-coherent memory;
+    // done_dev is its device address); issued_tag[p] = the tag of the last fragment launch that read
+    // set p (0: none); last_tag / last_stream = the previous fragment launch
+    volatile uint32_t *done_host = nullptr;
+    uint32_t *done_dev = nullptr;
+    uint32_t issued_tag[kSets] = {}, last_tag = 0;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t handoff = nullptr;
     uint32_t frame_no = 0;                     // frames issued: set frame_no % kSets
     uint32_t *frame = nullptr;
     size_t frame_cap = 0;
@@ -264,6 +273,14 @@ void initialize() {
         HIPCHECK(hipEventCreateWithFlags(&g.geo_done[p], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&g.frag_done[p], hipEventDisableTiming));
     }
+    {
+        void *h = nullptr;
+        HIPCHECK(hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+        memset(h, 0, sizeof(uint32_t));
+        g.done_host = static_cast<volatile uint32_t *>(h);
+        HIPCHECK(hipHostGetDevicePointer((void **)&g.done_dev, h, 0));
+        HIPCHECK(hipEventCreateWithFlags(&g.handoff, hipEventDisableTiming));
+    }
     // geometry streams at the highest priority: their (small, latency-bound) workgroups are
     // dispatched as soon as the previous frame's fragment workgroups free a slot
     int prio_least = 0, prio_greatest = 0;
@@ -293,14 +310,17 @@ void release_all() {
             if (gs) (void)hipStreamSynchronize(gs);
         (void)hipDeviceSynchronize();
         unregister_all();
-        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.tris[0], g.tris[1], g.frame,
-                        g.rowtab[0], g.rowtab[1], g.binmask[0], g.binmask[1],
-                        g.tile_counts[0], g.tile_counts[1], g.tile_offs[0], g.tile_offs[1], g.tile_cursor[0],
-                        g.tile_cursor[1], g.tile_list[0], g.tile_list[1],  // tile_total aliases app_count
-                        g.recs[0], g.recs[1], g.boxes[0], g.boxes[1], g.app_list[0], g.app_list[1],
-                        g.app_count[0], g.app_count[1], g.keys};
+        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.frame, g.keys};
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
+        for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
+            void *set[] = {g.tris[q], g.rowtab[q], g.binmask[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
+                           g.tile_list[q], g.recs[q], g.boxes[q], g.app_list[q], g.app_count[q]};
+            for (void *p : set)
+                if (p) (void)hipFree(p);
+        }
+        if (g.done_host) (void)hipHostFree((void *)g.done_host);
+        if (g.handoff) (void)hipEventDestroy(g.handoff);
         if (g.tile_total_host) (void)hipHostFree(g.tile_total_host);
         for (int p = 0; p < kSets; p++) {
             if (g.geo_done[p]) (void)hipEventDestroy(g.geo_done[p]);
@@ -354,6 +374,29 @@ TimingSlot *timing_slot() {
 uint32_t next_set() {
     g.frame_no++;
     return g.frame_no % kSets;
+}
+
+// Row path: block until the last fragment kernel that read buffer set p has finished (its tag is in
+// done_host[p]).  Usually it has: the host runs at most kSets frames ahead of the GPU.
+// (the one after it has been issued already: the host waits here for frame k - kSets, and frames
+// k - kSets + 1 .. k - 1 were issued on the same stream; tags grow by frame)
+void wait_set_free(uint32_t p) {
+    const uint32_t want = g.issued_tag[p];
+    if (want == 0 || __atomic_load_n(g.done_host, __ATOMIC_ACQUIRE) >= want) return;
+    if (want == g.last_tag) {
+        // no row-path fragment launch after it to report it (tile-path frames followed): drain its stream
+        HIPCHECK(hipStreamSynchronize(g.last_stream));
+        __atomic_store_n(g.done_host, want, __ATOMIC_RELEASE);
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(g.done_host, __ATOMIC_ACQUIRE) < want) {
+        __builtin_ia32_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+            HIPCHECK(hipDeviceSynchronize());      // (never expected) surfaces a device fault
+            __atomic_store_n(g.done_host, g.last_tag, __ATOMIC_RELEASE);
+        }
+    }
 }
 
 // S3R_SERIAL (profiling): the geometry waits for every earlier fragment kernel -- no overlap.
@@ -466,8 +509,8 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
             if (g.binmask[p]) HIPCHECK(hipFree(g.binmask[p]));
-            g.binmask[p] = dalloc<uint32_t>(nmask);
-            HIPCHECK(hipMemset(g.binmask[p], 0, nmask * sizeof(uint32_t)));   // then kept zero by k_fragment
+            g.binmask[p] = dalloc<unsigned long long>(nmask);
+            HIPCHECK(hipMemset(g.binmask[p], 0, nmask * sizeof(unsigned long long)));   // tag 0: no frame
         }
         g.binmask_cap = nmask;
     }
@@ -476,19 +519,35 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     hipStream_t geo = g.geo[g.frame_no % kGeoStreams];
     hp.lap(1);
     // the set's last reader (frame k - kSets) has usually finished: then no cross-stream wait
-    if (g.serial || hipEventQuery(g.frag_done[p]) != hipSuccess) HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
-    if (g.serial) wait_all_fragments(geo);
+    if (g.serial) {
+        HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
+        wait_all_fragments(geo);
+    } else {
+        wait_set_free(p);
+    }
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     hp.lap(2);
+    const uint32_t tag = g.frame_no;              // >= 1: frame k's tag for its slot masks and completion
     launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], geo, g.geo_done[p]);
+                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], tag, geo, g.geo_done[p]);
     hp.lap(3);
     // fragment on the caller's stream
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
+    // completion: the kernel's last workgroup writes the frame's tag into host memory (wait_set_free);
+    // the event only where S3R_SERIAL waits on it
+    if (g.last_stream && st != g.last_stream) {
+        // a new caller stream: order it after the previous fragment launch (the completion chain of
+        // wait_set_free assumes one stream)
+        HIPCHECK(hipEventRecord(g.handoff, g.last_stream));
+        HIPCHECK(hipStreamWaitEvent(st, g.handoff, 0));
+    }
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.binmask[p], st, g.frag_done[p]);
+                    g.binmask[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag);
+    g.issued_tag[p] = tag;
+    g.last_tag = tag;
+    g.last_stream = st;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipGetLastError());
     hp.lap(5);
@@ -623,6 +682,13 @@ __attribute__((visibility("default"))) void s3r_stats(uint64_t out[16], int rese
 // number of workgroups copied (0 in the product build).
 __attribute__((visibility("default"))) uint32_t s3r_stats_wg_times(uint64_t *out, uint32_t max_wg) {
     return wg_times_read(reinterpret_cast<unsigned long long *>(out), max_wg);
+}
+
+// Timing build only (-DS3R_WGTIME): per k_geometry workgroup (slot + row block * 2T) of the launches since the
+// last call, 100 MHz wall clock: out[4 * wg + k], k = 0 start, 1 slot set up, 2 bins set, 3 end.  Returns
+// the number of workgroup records copied (0 in the product build) and clears them.
+__attribute__((visibility("default"))) uint32_t s3r_stats_geo_times(uint64_t *out, uint32_t max_wg) {
+    return geo_times_read(reinterpret_cast<unsigned long long *>(out), max_wg);
 }
 
 // Stats build only: k_geometry wall-clock profile (100 MHz ticks): {max setup time of a workgroup,

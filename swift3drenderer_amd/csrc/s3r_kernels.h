@@ -10,11 +10,13 @@ namespace s3r {
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *binmask, hipStream_t st, hipEvent_t done);
+                     uint32_t rows_local, const unsigned long long *binmask, uint32_t tag, hipStream_t st,
+                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their slot masks:
-// fragment_bins() masks of bin_words(nslots) u32 each, all zero between frames (the fragment kernel
-// clears what k_geometry sets).
+// fragment_bins() masks of bin_words(nslots) tagged words each: (frame tag << 32) | 32 slot bits, a
+// word whose tag is not the frame's reads as empty -- nothing clears them (k_fragment only reads the
+// buffer set, so a set is reusable as soon as its last fragment kernel has counted out).
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
 uint32_t bin_words(uint32_t nslots);
 
@@ -25,7 +27,8 @@ uint32_t start_entries(uint32_t W);
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, uint32_t *binmask, hipStream_t st, hipEvent_t done);
+                     TriSetup *tris, float *rowtab, unsigned long long *binmask, uint32_t tag, hipStream_t st,
+                     hipEvent_t done);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
@@ -55,6 +58,7 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
 
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);
+uint32_t geo_times_read(unsigned long long *out, uint32_t max_wg);
 
 int fastmath_test(uint32_t mode, uint64_t count, uint64_t out[2]);
 void launch_walk_test(const float *s, const float *d, const uint32_t *n, float *out, uint32_t *lin, float *del,
