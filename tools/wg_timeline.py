@@ -70,6 +70,8 @@ def main():
               f'list length mean {t[m, 7].mean():.1f} max {t[m, 7].max()}')
         print(f'      per workgroup (wave 0): slow-path chunks {t[m, 8].mean():.2f}, non-linear chunks {t[m, 9].mean():.2f}, '
               f'live triangles tested {t[m, 10].mean():.2f}')
+    if os.environ.get('S3R_WGT_DUMP'):
+        np.save(os.environ['S3R_WGT_DUMP'], t)
     edges = np.linspace(0, span, 11)
     live = [int(((rel[:, 0] <= e) & (rel[:, 3] > e)).sum()) for e in edges[:-1]]
     print('  in flight at 0%,10%..90% of the span:', live)
