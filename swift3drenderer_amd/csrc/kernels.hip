@@ -1111,26 +1111,45 @@ __device__ __forceinline__ TileSpan box_tiles(uint32_t bx, uint32_t by, uint32_t
 
 // Every lane adds 1 to counter[key] for each tile of its span (or nothing); lanes of the wave with
 // the same key share one atomic.  With `list`, the returned positions place `slot` in the lists.
+// Per step the groups are found first (ballots only), then every group leader issues its atomic in
+// ONE vector instruction, so a step waits for one atomic round trip, not one per distinct tile.
 __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x, uint32_t *__restrict__ ctr,
                                            uint32_t *__restrict__ list, uint32_t slot) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t rounds = sp.n;
     for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
-    for (uint32_t k = 0; k < rounds; k++) {
-        const bool act = k < sp.n;
-        const uint32_t key = act ? (sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx : 0xFFFFFFFFu;
-        uint64_t todo = __ballot(act);
-        while (todo) {
-            const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-            const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
-            const uint64_t grp = __ballot(act && key == lk);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&ctr[lk], (uint32_t)__builtin_popcountll(grp));
-            if (list) {
-                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
-                if (act && key == lk) list[base + lane_prefix(grp, lane)] = slot;
+    constexpr uint32_t kSteps = 4;                       // steps whose atomics are in flight together
+    for (uint32_t k0 = 0; k0 < rounds; k0 += kSteps) {
+        uint32_t key[kSteps], leader_of[kSteps], rank[kSteps], base[kSteps];
+#pragma unroll
+        for (uint32_t q = 0; q < kSteps; q++) {
+            const uint32_t k = k0 + q;
+            const bool act = k < sp.n;
+            key[q] = act ? (sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx : 0xFFFFFFFFu;
+            uint64_t todo = __ballot(act);
+            uint32_t my_leader = 0, my_rank = 0, cnt = 0;
+            while (todo) {
+                const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+                const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key[q], (int)leader);
+                const uint64_t grp = __ballot(act && key[q] == lk);
+                if (act && key[q] == lk) { my_leader = leader; my_rank = lane_prefix(grp, lane); }
+                if (lane == leader) cnt = (uint32_t)__builtin_popcountll(grp);
+                todo &= ~grp;
             }
-            todo &= ~grp;
+            leader_of[q] = my_leader;
+            rank[q] = my_rank;
+            base[q] = 0;
+            if (act && lane == my_leader) {
+                if (list) base[q] = atomicAdd(&ctr[key[q]], cnt);
+                else atomicAdd(&ctr[key[q]], cnt);
+            }
+        }
+        if (list) {
+#pragma unroll
+            for (uint32_t q = 0; q < kSteps; q++) {
+                const uint32_t b = (uint32_t)__shfl((int)base[q], (int)leader_of[q]);
+                if (k0 + q < sp.n) list[b + rank[q]] = slot;
+            }
         }
     }
 }
