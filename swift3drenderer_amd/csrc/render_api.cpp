@@ -88,7 +88,8 @@ struct Lib {
     // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
     // fragment launch on its stream (complete by stream order) in *done_host (host-coherent memory;
     // done_dev is its device address); issued_tag[p] = the tag of the last fragment launch that read
-    // set p (0: none); last_tag / last_stream = the previous fragment launch
+    // set p (0: none); last_tag = the previous row-path fragment launch, last_stream = the stream of
+    // the previous frame (either path)
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
@@ -399,6 +400,17 @@ void wait_set_free(uint32_t p) {
     }
 }
 
+// Frames are ordered on the caller's stream.  When a frame arrives on another stream than the
+// previous one, that stream first waits for the previous frame's fragment stage (one event): the
+// row path's completion chain (wait_set_free) and the tile path's shared key buffer assume it.
+void follow_previous_frame(hipStream_t st) {
+    if (g.last_stream && st != g.last_stream) {
+        HIPCHECK(hipEventRecord(g.handoff, g.last_stream));
+        HIPCHECK(hipStreamWaitEvent(st, g.handoff, 0));
+    }
+    g.last_stream = st;
+}
+
 // S3R_SERIAL (profiling): the geometry waits for every earlier fragment kernel -- no overlap.
 void wait_all_fragments(hipStream_t geo) {
     for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[q], 0));
@@ -475,6 +487,7 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
     launch_tile_fill(g.boxes[p], g.ntri, g.recs[p], g.app_list[p], napp, W, band, nparts, part, g.tile_cursor[p],
                      g.tile_list[p], geo);
     HIPCHECK(hipEventRecord(g.geo_done[p], geo));
+    follow_previous_frame(st);
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_tile_raster(g.recs[p], W, band, nparts, part, rows_local, g.tile_offs[p], g.tile_counts[p], g.tile_list[p],
@@ -537,17 +550,11 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     // completion: the kernel's last workgroup writes the frame's tag into host memory (wait_set_free);
     // the event only where S3R_SERIAL waits on it
-    if (g.last_stream && st != g.last_stream) {
-        // a new caller stream: order it after the previous fragment launch (the completion chain of
-        // wait_set_free assumes one stream)
-        HIPCHECK(hipEventRecord(g.handoff, g.last_stream));
-        HIPCHECK(hipStreamWaitEvent(st, g.handoff, 0));
-    }
+    follow_previous_frame(st);
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     g.binmask[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag);
     g.issued_tag[p] = tag;
     g.last_tag = tag;
-    g.last_stream = st;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipGetLastError());
     hp.lap(5);

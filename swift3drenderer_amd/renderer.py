@@ -20,6 +20,9 @@ EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_set_raster_p
            's3r_render_bands', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
 
 _lib = None
+# host frames of update_and_render(out=None), one per shape, kept for the process: the library may
+# hold a hipHostRegister registration on them (render_api.cpp host_pinned)
+_HOST_FRAMES: dict = {}
 
 
 def load_library(path: str = LIB_PATH):
@@ -73,13 +76,21 @@ class Renderer:
         self.lib.s3r_configure(data_path.encode() if data_path else None, device)
 
     def update_and_render(self, width: int, height: int, inp, out: np.ndarray | None = None) -> np.ndarray:
-        """updateAndRender into a host uint32 (H, W) buffer (the reference's contract)."""
-        if out is None:
-            out = np.empty((height, width), dtype=np.uint32)
+        """updateAndRender into a host uint32 (H, W) buffer (the reference's contract).
+
+        The library may page-lock (hipHostRegister) the caller's buffer and keeps that registration
+        for the buffer's pointer, like the reference app's long-lived double buffer (main.swift:117):
+        a caller passing `out` keeps it alive while it uses the library.  Without `out` the frame goes
+        through a buffer this object owns, and a copy is returned."""
+        own = out is None
+        if own:
+            out = _HOST_FRAMES.get((height, width))
+            if out is None:
+                out = _HOST_FRAMES[(height, width)] = np.empty((height, width), dtype=np.uint32)
         pd = pixel_data_for(out)
         i = Input.of(inp)
         self.lib.updateAndRender(ctypes.byref(pd), ctypes.byref(i))
-        return out
+        return out.copy() if own else out
 
     def render_bands(self, inp, width: int, height: int, band: int, nparts: int, part: int, dev_ptr: int,
                      stream: int = 0) -> int:

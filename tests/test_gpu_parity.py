@@ -81,3 +81,44 @@ def test_long_walk_sequence(gpu_renderer, scene_dir):
         want = o.update_and_render(480, 320, inp)
         got = gpu_renderer.update_and_render(480, 320, inp)
         assert np.array_equal(got, want), f'frame {k} {inp}: ' + diff_report(got, want)
+
+
+def test_pipelined_frames_on_mixed_streams(gpu_renderer, scene_dir):
+    """Frames issued without waiting (more in flight than the 4 buffer sets), alternating between two
+    caller streams, with tile-path frames and a host-buffer updateAndRender in between: every frame
+    equals the oracle's frame for the same input sequence.  Exercises the event-free buffer-set reuse
+    (render_api.cpp wait_set_free), the stream hand-off and the row/tile path switch."""
+    import torch
+    from oracle.oracle import OracleRenderer
+    path = scene_dir['full']
+    o = OracleRenderer(path)
+    gpu_renderer.configure(path)
+    W, H = 320, 240
+    rng = np.random.default_rng(11)
+    inputs, wants = [], []
+    mouse = np.array([0.0, -120.0])
+    for k in range(18):                      # the oracle first, so the GPU frames go out back to back
+        keys = rng.integers(0, 2, 4) * rng.uniform(0, 10, 4)
+        mouse += rng.normal(0, 12, 2)
+        inputs.append((*keys, *mouse))
+        wants.append(o.update_and_render(W, H, inputs[-1]))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = []
+    for k, inp in enumerate(inputs):
+        if k == 7:
+            gpu_renderer.set_raster_path('tiles')
+        if k == 10:
+            gpu_renderer.set_raster_path('auto')
+        if k == 13:
+            got = gpu_renderer.update_and_render(W, H, inp)          # host buffer, the library's own stream
+            assert np.array_equal(got, wants[k]), f'frame {k} (updateAndRender): ' + diff_report(got, wants[k])
+            continue
+        buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
+        st = streams[(k // 3) % 2]
+        with torch.cuda.stream(st):
+            gpu_renderer.render_bands(inp, W, H, H, 1, 0, buf.data_ptr(), st.cuda_stream)
+        bufs.append((k, buf))
+    torch.cuda.synchronize()
+    for k, buf in bufs:
+        got = buf.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, wants[k]), f'frame {k}: ' + diff_report(got, wants[k])
