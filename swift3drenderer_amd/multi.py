@@ -34,16 +34,22 @@ class BandGather:
         self.recv = None
         self.frame = None
         if rank == 0:
-            self.recv = [torch.empty((self.max_rows, width), dtype=torch.int32, device=device) for _ in range(world)]
+            # one contiguous receive buffer (part p's rows at [p * max_rows, ...)) and, per frame row,
+            # its row in that buffer: the de-interleave is then ONE row gather (index_select)
+            self.recv_all = torch.empty((world * self.max_rows, width), dtype=torch.int32, device=device)
+            self.recv = [self.recv_all[p * self.max_rows:(p + 1) * self.max_rows] for p in range(world)]
             self.frame = torch.empty((height, width), dtype=torch.int32, device=device)
-            self.ids = [torch.as_tensor(band_row_ids(height, band, world, p), device=device) for p in range(world)]
+            src = np.empty(height, dtype=np.int64)
+            for p in range(world):
+                ids = band_row_ids(height, band, world, p)
+                src[ids] = p * self.max_rows + np.arange(len(ids))
+            self.src_rows = torch.as_tensor(src, device=device)
 
     def gather(self, group=None):
         """Collective: every rank's `send` (rows [0, rows) valid) -> rank 0's `frame`."""
         dist.gather(self.send, self.recv, dst=0, group=group)
         if self.rank == 0:
-            for p in range(self.N):
-                self.frame.index_copy_(0, self.ids[p], self.recv[p][: self.ids[p].numel()])
+            torch.index_select(self.recv_all, 0, self.src_rows, out=self.frame)
         return self.frame
 
 
