@@ -68,8 +68,11 @@ int s3r_raster_path(void);
  * resize semantics as updateAndRender.  Frame row y belongs to part ((y / band_rows) % n_parts);
  * this part's rows are written compactly, in increasing y, to the DEVICE buffer dev_out
  * (rows_local x width u32), asynchronously on `stream` (a hipStream_t; NULL = the default (null)
- * stream).  The geometry stage runs on an internal stream and is ordered with `stream` by events,
- * so frame k+1's geometry overlaps frame k's fragment kernel.  n_parts = 1 renders the whole
+ * stream).  The geometry stage runs on internal streams and is ordered before this frame's
+ * fragment stage by an event, so later frames' geometry overlaps earlier frames' fragment kernels.
+ * Frames are ordered: a frame issued on another stream than the previous frame first waits for the
+ * previous frame's fragment stage.  The call returns without waiting for the GPU unless the host is
+ * 4 frames ahead (it then waits for the oldest frame's buffers).  n_parts = 1 renders the whole
  * frame.  Returns rows_local, or -1 on bad arguments. */
 int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height, uint32_t band_rows,
                          uint32_t n_parts, uint32_t part, uint32_t *dev_out, void *stream);
