@@ -43,7 +43,9 @@ def build_variant(tag: str, defines: dict, verbose: bool = False) -> str:
     bdir = os.path.join(BUILD, tag)
     os.makedirs(bdir, exist_ok=True)
     lib_path = os.path.join(BUILD, f'librender_{tag}.so')
-    extra = [f'-D{k}={v}' for k, v in defines.items()]
+    extra = [f'-D{k}={v}' for k, v in defines.items() if not k.startswith('-')]
+    extra += [k for k in defines if k.startswith('-')]          # raw compiler flags: {"-mllvm -x=y": 1}
+    extra = [a for e in extra for a in (e.split(' ') if e.startswith('-mllvm') else [e])]
     objs = []
     for src in SOURCES:
         o = os.path.join(bdir, src + '.o')

@@ -15,6 +15,9 @@ sys.path.insert(0, ROOT)
 import json
 
 # S3R_VARIANTS='{"tag": {"MACRO": value, ...}, ...}' overrides the default set
+# (or S3R_VARIANTS_FILE=<path of such a JSON file>)
+if os.environ.get('S3R_VARIANTS_FILE'):
+    os.environ['S3R_VARIANTS'] = open(os.environ['S3R_VARIANTS_FILE']).read()
 VARIANTS = json.loads(os.environ['S3R_VARIANTS']) if os.environ.get('S3R_VARIANTS') else {
     'base': {},
     'st64': {'S3R_TSTAGE': 64},
