@@ -122,3 +122,69 @@ def test_pipelined_frames_on_mixed_streams(gpu_renderer, scene_dir):
     for k, buf in bufs:
         got = buf.cpu().numpy().view(np.uint32)
         assert np.array_equal(got, wants[k]), f'frame {k}: ' + diff_report(got, wants[k])
+
+
+def test_empty_scene(gpu_renderer, tmp_path):
+    """A data.bin without triangles (or textures): every pixel is the background (render.cpp:282)."""
+    from swift3drenderer_amd import scene
+    path = str(tmp_path / 'empty.bin')
+    scene.write_scene(scene.Scene(), path)
+    script = poses.script('P_over')
+    want = oracle_render_pose(path, script, 160, 120)
+    got = render_pose(gpu_renderer, path, script, 160, 120)
+    assert np.array_equal(got, want), diff_report(got, want)
+    assert (got == 0x1E1E1E).all()
+
+
+@pytest.mark.parametrize('w,h', [(1, 1), (1, 300), (300, 1), (65, 2), (2, 65), (385, 7)])
+def test_thin_frames(gpu_renderer, scene_dir, w, h):
+    """Single-pixel, single-row and single-column frames; widths just past a chunk / a segment."""
+    script = poses.script('P_over')
+    want = oracle_render_pose(scene_dir['full'], script, w, h)
+    got = render_pose(gpu_renderer, scene_dir['full'], script, w, h)
+    assert np.array_equal(got, want), diff_report(got, want)
+
+
+def test_nothing_visible(gpu_renderer, scene_dir):
+    """Camera turned away from every triangle (all culled off screen, render.cpp:312-315)."""
+    script = [(0, 0, 0, 0, 4000.0, 0.0), (0, 0, 0, 0, 8000.0, 0.0)]
+    want = oracle_render_pose(scene_dir['full'], script, 320, 240)
+    got = render_pose(gpu_renderer, scene_dir['full'], script, 320, 240)
+    assert np.array_equal(got, want), diff_report(got, want)
+
+
+def stacked_quads_scene(path, n=160):
+    """n coloured quads (2n triangles) stacked in front of the identity camera, slightly shifted and
+    tilted so that their depths interleave; every 10th repeats the previous depth (tie order)."""
+    from swift3drenderer_amd import scene
+    sc = scene.Scene()
+    rng = np.random.default_rng(3)
+    z = -5.0
+    for i in range(n):
+        if i % 10:
+            z -= 0.05
+        dx, dy, tilt = rng.uniform(-0.6, 0.6), rng.uniform(-0.4, 0.4), rng.uniform(-0.3, 0.3)
+        k = len(sc.vertices)
+        sc.vertices += [scene.v3(-4 + dx, -3 + dy, z - tilt), scene.v3(4 + dx, -3 + dy, z + tilt),
+                        scene.v3(-4 + dx, 3 + dy, z - tilt), scene.v3(4 + dx, 3 + dy, z + tilt)]
+        sc.vertex_indexes += [k, k + 2, k + 1, k + 1, k + 2, k + 3]
+        j = len(sc.attributes)
+        cols = [tuple(float(c) for c in rng.uniform(0, 255, 3)) for _ in range(4)]
+        nrm = scene.v3(0, 0, 1)
+        sc.attributes += [(nrm, ("c", scene.v3(*cols[q]))) for q in (0, 2, 1, 1, 2, 3)]
+        sc.attribute_indexes += list(range(j, j + 6))
+    scene.write_scene(sc, path)
+
+
+def test_row_path_list_overflow(gpu_renderer, tmp_path):
+    """320 stacked triangles cover every fragment workgroup: more than the 128 a workgroup lists from
+    the geometry's slot masks, so the row path takes its in-kernel slot-scan rounds (build_list)."""
+    path = str(tmp_path / 'stack.bin')
+    stacked_quads_scene(path)
+    for w, h in ((320, 240), (1280, 720)):
+        ident = [(0, 0, 0, 0, 0, 0)]
+        want = oracle_render_pose(path, ident, w, h)
+        got = render_pose(gpu_renderer, path, ident, w, h)
+        assert gpu_renderer.raster_path() == 'rows'
+        assert (want != 0x1E1E1E).mean() > 0.5
+        assert np.array_equal(got, want), f'{w}x{h}: ' + diff_report(got, want)
