@@ -86,7 +86,7 @@ struct Lib {
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
     // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
-    // fragment launch on its stream (complete by stream order) in *done_host (host-coherent memory;
+    // fragment launch (complete by stream order) in *done_host (host-coherent memory;
     // done_dev is its device address); issued_tag[p] = the tag of the last fragment launch that read
     // set p (0: none); last_tag = the previous row-path fragment launch, last_stream = the stream of
     // the previous frame (either path)
@@ -377,10 +377,11 @@ uint32_t next_set() {
     return g.frame_no % kSets;
 }
 
-// Row path: block until the last fragment kernel that read buffer set p has finished (its tag is in
-// done_host[p]).  Usually it has: the host runs at most kSets frames ahead of the GPU.
-// (the one after it has been issued already: the host waits here for frame k - kSets, and frames
-// k - kSets + 1 .. k - 1 were issued on the same stream; tags grow by frame)
+// Row path: block until the last fragment kernel that read buffer set p has finished.  *done_host
+// holds the tag of the newest fragment launch known complete: every launch's first workgroup stores
+// its predecessor's tag there, and tags grow by frame.  Usually the set is free (the host runs at
+// most kSets frames ahead of the GPU); otherwise the launch after it -- issued already, in order on
+// the same stream -- reports it when it starts.
 void wait_set_free(uint32_t p) {
     const uint32_t want = g.issued_tag[p];
     if (want == 0 || __atomic_load_n(g.done_host, __ATOMIC_ACQUIRE) >= want) return;
@@ -544,13 +545,13 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, g.tris[p], g.rowtab[p], g.binmask[p], tag, geo, g.geo_done[p]);
     hp.lap(3);
-    // fragment on the caller's stream
+    // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
+    // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
+    // only where S3R_SERIAL waits on it
+    follow_previous_frame(st);
     HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
     hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    // completion: the kernel's last workgroup writes the frame's tag into host memory (wait_set_free);
-    // the event only where S3R_SERIAL waits on it
-    follow_previous_frame(st);
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     g.binmask[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag);
     g.issued_tag[p] = tag;
