@@ -153,9 +153,10 @@ def test_nothing_visible(gpu_renderer, scene_dir):
     assert np.array_equal(got, want), diff_report(got, want)
 
 
-def stacked_quads_scene(path, n=160):
+def stacked_quads_scene(path, n=160, size=1.0):
     """n coloured quads (2n triangles) stacked in front of the identity camera, slightly shifted and
-    tilted so that their depths interleave; every 10th repeats the previous depth (tie order)."""
+    tilted so that their depths interleave; every 10th repeats the previous depth (tie order).
+    size = 1 fills the view; smaller quads cover the centre."""
     from swift3drenderer_amd import scene
     sc = scene.Scene()
     rng = np.random.default_rng(3)
@@ -163,10 +164,12 @@ def stacked_quads_scene(path, n=160):
     for i in range(n):
         if i % 10:
             z -= 0.05
-        dx, dy, tilt = rng.uniform(-0.6, 0.6), rng.uniform(-0.4, 0.4), rng.uniform(-0.3, 0.3)
+        dx, dy, tilt = (rng.uniform(-0.6, 0.6) * size, rng.uniform(-0.4, 0.4) * size,
+                        rng.uniform(-0.3, 0.3) * size)
+        a, b = 4 * size, 3 * size
         k = len(sc.vertices)
-        sc.vertices += [scene.v3(-4 + dx, -3 + dy, z - tilt), scene.v3(4 + dx, -3 + dy, z + tilt),
-                        scene.v3(-4 + dx, 3 + dy, z - tilt), scene.v3(4 + dx, 3 + dy, z + tilt)]
+        sc.vertices += [scene.v3(-a + dx, -b + dy, z - tilt), scene.v3(a + dx, -b + dy, z + tilt),
+                        scene.v3(-a + dx, b + dy, z - tilt), scene.v3(a + dx, b + dy, z + tilt)]
         sc.vertex_indexes += [k, k + 2, k + 1, k + 1, k + 2, k + 3]
         j = len(sc.attributes)
         cols = [tuple(float(c) for c in rng.uniform(0, 255, 3)) for _ in range(4)]
@@ -188,3 +191,38 @@ def test_row_path_list_overflow(gpu_renderer, tmp_path):
         assert gpu_renderer.raster_path() == 'rows'
         assert (want != 0x1E1E1E).mean() > 0.5
         assert np.array_equal(got, want), f'{w}x{h}: ' + diff_report(got, want)
+
+
+def _parts_vs_oracle(r, path, script, W, H, nparts, band, parts):
+    import torch
+    from swift3drenderer_amd.multi import band_row_ids
+    want = oracle_render_pose(path, script, W, H)
+    r.configure(path)
+    dev = torch.device('cuda', 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    hold = (0, 0, 0, 0) + tuple(script[-1][4:6])
+    scratch = torch.empty((H, W), dtype=torch.int32, device=dev)
+    for t in script:                                         # the script's camera, one frame each
+        r.render_bands(t, W, H, band, nparts, 0, scratch.data_ptr(), st)
+    torch.cuda.synchronize()
+    for p in parts:
+        ids = band_row_ids(H, band, nparts, p)
+        buf = torch.full((max(len(ids), 1), W), -1, dtype=torch.int32, device=dev)
+        n = r.render_bands(hold, W, H, band, nparts, p, buf.data_ptr(), st)
+        assert n == len(ids)
+        got = buf.cpu().numpy().view(np.uint32)[:n]
+        assert np.array_equal(got, want[ids]), f'part {p} of {nparts}: ' + diff_report(got, want[ids])
+
+
+def test_small_parts_match_oracle(gpu_renderer, scene_dir):
+    """Every GPU's rows of an 8-way 4K split (128-px fragment segments at this size): each part is
+    bit-identical to the oracle's rows of the whole frame."""
+    _parts_vs_oracle(gpu_renderer, scene_dir['full'], poses.script('P_over'), 3840, 2160, 8, 16, range(8))
+
+
+def test_small_parts_overflow(gpu_renderer, tmp_path):
+    """The list-overflow rounds (more than 128 triangles per workgroup) in one GPU's rows of an
+    8-way 4K split."""
+    path = str(tmp_path / 'stack-small.bin')
+    stacked_quads_scene(path, size=0.08)
+    _parts_vs_oracle(gpu_renderer, path, [(0, 0, 0, 0, 0, 0)], 3840, 2160, 8, 16, (0, 5))
