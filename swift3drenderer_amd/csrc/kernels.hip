@@ -132,15 +132,9 @@ __device__ __forceinline__ bool raster_part(const Vert d[3], float sw, float sh,
     return true;
 }
 
-// render.cpp:311-359 for one (possibly clipped) triangle.
-__device__ __forceinline__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, TriSetup *out) {
-    TriSetup t;
-    t.kind = kDead;
-    t.pad0 = t.pad1 = 0;
-    if (!raster_part(d, sw, sh, t)) {
-        out->kind = kDead;
-        return;
-    }
+// render.cpp:337-352, the shading constants, from the raster part's 1/z per corner and steps
+// (t.rvz, t.dx, t.dy).
+__device__ __forceinline__ void shading_part(const Vert d[3], bool textured, TriSetup &t) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const float r = t.rvz[k];
@@ -172,6 +166,18 @@ __device__ __forceinline__ void setup_tri(const Vert d[3], bool textured, float 
         t.col[4] = u2; t.col[5] = v2; t.col[6] = dzx; t.col[7] = dzy;
         t.col[8] = tx; t.col[9] = ty; t.col[10] = t.col[11] = 0.0f;
     }
+}
+
+// render.cpp:311-359 for one (possibly clipped) triangle.
+__device__ __forceinline__ void setup_tri(const Vert d[3], bool textured, float sw, float sh, TriSetup *out) {
+    TriSetup t;
+    t.kind = kDead;
+    t.pad0 = t.pad1 = 0;
+    if (!raster_part(d, sw, sh, t)) {
+        out->kind = kDead;
+        return;
+    }
+    shading_part(d, textured, t);
     *out = t;
 }
 
@@ -1536,7 +1542,32 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
         const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
         const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
         TriSetup ts;
-        slot_setup(s, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, sw, sh, ts);
+        // the winner's shading constants: corners transformed again (render.cpp:286, :291); an
+        // unclipped triangle takes its 1/z and steps from its raster record (the same values
+        // k_tile_setup computed), a clipped one is set up in full
+        const uint32_t t = s < ntri ? s : s - ntri;
+        Vert d[3];
+        bool near_cut = false;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint32_t ai = aidx[3 * t + c];
+            const F3 cv = mat_mul(m, vtx[vidx[3 * t + c]]);
+            const float nz = -cv.z;
+            d[c].cv = cv;
+            d[c].rv = mk3(0.0f, 0.0f, (0.0f * factor) / nz + nz);                 // :288 (z only)
+            d[c].n = mat_mul(m, nrm[ai]);
+            d[c].pay = pay[ai];
+            near_cut = near_cut || d[c].rv.z < kNear;
+        }
+        if (s >= ntri || near_cut) {
+            slot_setup(s, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, sw, sh, ts);
+        } else {
+            ts.kind = kDead;
+            ts.rvz[0] = q3.y; ts.rvz[1] = q3.z; ts.rvz[2] = q3.w;
+            ts.dx[0] = q1.w; ts.dx[1] = q2.x; ts.dx[2] = q2.y;
+            ts.dy[0] = q2.z; ts.dy[1] = q2.w; ts.dy[2] = q3.x;
+            shading_part(d, disc[aidx[3 * t]] != 0, ts);
+        }
         v = shade(&ts, w0, w1, w2, ooz, tex, ntex);
     }
     out[idx] = v;
