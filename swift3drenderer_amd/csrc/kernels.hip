@@ -282,6 +282,9 @@ __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint
     const uint32_t y = u32_of_float(frac1(v) * (float)ly) + (511u & ~(2u * ly - 1u));
     const uint32_t off = (x + (y << 9)) & (kTexTexels - 1u);
     // Out-of-range texture index is UB in the reference; defined here (and in the oracle) as 0.
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 256)
+    return off * 0x010101u + base;                 // ablation: no texel load
+#endif
     return (base < ntex && ntex - base >= kTexTexels) ? tex[base + off] : 0u;
 }
 
@@ -618,12 +621,73 @@ S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float
     return rgb_pack(s * col.x, s * col.y, s * col.z);
 }
 
+#ifndef S3R_SHADE_FLAT
+#define S3R_SHADE_FLAT 1
+#endif
+#ifndef S3R_TEX_EARLY
+#define S3R_TEX_EARLY 1
+#endif
+// shade_core as one straight-line block: every correctly rounded division and sqrt takes its trimmed
+// sequence unconditionally while the range conditions are collected in `ok`; a lane with any operand
+// out of range is shaded again by shade_core (same bits either way).  Without the per-operation
+// branches the scheduler interleaves the independent chains (the normalisations of P and N, the
+// texture coordinates and the texel load; a colour triangle's lanes compute the texture path too and
+// discard it, its texel index is masked in range).
+S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0,
+                                    float4 k1, float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1,
+                                    float w2, float ooz, const uint32_t *__restrict__ tex, uint32_t ntex) {
+    bool ok = div_in_range(w0, ooz) & div_in_range(w1, ooz) & div_in_range(w2, ooz);
+    const float r = div_recip(ooz);
+    const float a = div_with_recip(w0, ooz, r), b = div_with_recip(w1, ooz, r), c = div_with_recip(w2, ooz, r);
+    // texture coordinates first: the texel load overlaps the normalisations
+    const float mu = (k0.x * a + k0.z * b) + k1.x * c;
+    const float mv = (k0.y * a + k0.w * b) + k1.y * c;
+    const float dvx = fabsf(k2.x - mu * k1.z), dvy = fabsf(k2.y - mv * k1.w);
+    const bool texd = kind != kColour;
+    ok &= !texd | (div_in_range(ooz, dvx) & div_in_range(ooz, dvy));
+    const float lvx = div_with_recip(ooz, dvx, div_recip(dvx));
+    const float lvy = div_with_recip(ooz, dvy, div_recip(dvy));
+#if S3R_TEX_EARLY
+    const uint32_t rgb = texel(tex, ntex, tex_base, mu, mv, lvx, lvy);
+#endif
+    auto norm = [&ok](F3 v) {
+        const float d = dot3(v, v);
+        ok &= sqrt_in_range_ok(d);
+        const float sq = sqrt_in_range(d);
+        const float inv = div_with_recip(1.0f, sq, div_recip(sq));
+        return mk3(v.x * inv, v.y * inv, v.z * inv);
+    };
+    const F3 P = mk3((c0.x * a + c1.x * b) + c2.x * c, (c0.y * a + c1.y * b) + c2.y * c,
+                     (c0.z * a + c1.z * b) + c2.z * c);
+    const F3 N = mk3((n0.x * a + n1.x * b) + n2.x * c, (n0.y * a + n1.y * b) + n2.y * c,
+                     (n0.z * a + n1.z * b) + n2.z * c);
+    const F3 pn = norm(P);
+    const F3 normal = norm(N);
+    const F3 point = mk3(-pn.x, -pn.y, -pn.z);
+    const F3 halfway = norm(add3(point, normal));
+    const float s = dot3(halfway, normal);
+#if !S3R_TEX_EARLY
+    const uint32_t rgb = texel(tex, ntex, tex_base, mu, mv, lvx, lvy);
+#endif
+    const F3 col = texd ? mk3((float)(rgb >> 16), (float)((rgb >> 8) & 255u), (float)(rgb & 255u))
+                        : mk3((k0.x * a + k1.x * b) + k2.x * c, (k0.y * a + k1.y * b) + k2.y * c,
+                              (k0.z * a + k1.z * b) + k2.z * c);
+    uint32_t res = rgb_pack(s * col.x, s * col.y, s * col.z);
+    if (!ok) res = shade_core(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, w0, w1, w2, ooz, tex, ntex);
+    return res;
+}
+
 // The same from a TriSetup record (tile path: a register-resident record).
 S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
                           const uint32_t *__restrict__ tex, uint32_t ntex) {
     const float4 *q = reinterpret_cast<const float4 *>(tp);
+#if S3R_SHADE_FLAT
+    return shade_core_flat(q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], tp->kind, tp->tex_base, w0, w1,
+                           w2, ooz, tex, ntex);
+#else
     return shade_core(q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], tp->kind, tp->tex_base, w0, w1, w2,
                       ooz, tex, ntex);
+#endif
 }
 
 // Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle.
@@ -1021,7 +1085,11 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                 row[xp] = win[p] < 0 ? kBackground : (uint32_t)win[p] ^ __float_as_uint(bw0[p] + bw1[p] + bw2[p] + depth[p]);
 #else
             if (row_ok && xp <= xe)
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 512)     // ablation: every shade reads one record
+                row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+#else
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+#endif
 #endif
         }
         S3R_WGC_ADD(2);
