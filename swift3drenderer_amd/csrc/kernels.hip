@@ -276,8 +276,12 @@ __device__ unsigned long long g_gwt[kGeoTimesMax * 4];
 __device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t base,
                                           float u, float v, float lvx, float lvy) {
     // getTextureColor, render.cpp:124-132
-    const uint32_t lx = next_power_of_two(u32_of_float(fmaxf(fminf(lvx, 256.f), 1.f)));
-    const uint32_t ly = next_power_of_two(u32_of_float(fmaxf(fminf(lvy, 256.f), 1.f)));
+    // levels clamped to [1, 256] (fminf(NaN, 256) = 256): the truncation needs no range guard and
+    // nextPowerOfTwo of i in [1, 256] is 1 << (32 - clz(i - 1)) for i > 1
+    const uint32_t ix = (uint32_t)(int32_t)fmaxf(fminf(lvx, 256.f), 1.f);
+    const uint32_t iy = (uint32_t)(int32_t)fmaxf(fminf(lvy, 256.f), 1.f);
+    const uint32_t lx = ix > 1u ? 1u << (32u - (uint32_t)__builtin_clz(ix - 1u)) : 1u;
+    const uint32_t ly = iy > 1u ? 1u << (32u - (uint32_t)__builtin_clz(iy - 1u)) : 1u;
     const uint32_t x = u32_of_float(frac1(u) * (float)lx) + (511u & ~(2u * lx - 1u));
     const uint32_t y = u32_of_float(frac1(v) * (float)ly) + (511u & ~(2u * ly - 1u));
     const uint32_t off = (x + (y << 9)) & (kTexTexels - 1u);
@@ -564,36 +568,30 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
 #ifndef S3R_FASTDIV
 #define S3R_FASTDIV 1                  // shading: trimmed exact division / sqrt sequences in range
 #endif
-#if S3R_FASTDIV
-#define S3R_NORMALIZE fast_normalize3_dev
-#else
-#define S3R_NORMALIZE fast_normalize3
-#endif
 
 // Deferred shading of the winning triangle (render.cpp:366-371) from its constants: cvr (c0-c2),
 // nr (n0-n2), col (k0-k2), kind and texture base.
+template <bool kFast = (S3R_FASTDIV != 0)>
 S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0, float4 k1,
                                float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1, float w2, float ooz,
                                const uint32_t *__restrict__ tex, uint32_t ntex) {
     // w / (1/z), three quotients by one divisor: the refined reciprocal is shared (s3r_common.h)
     float a, b, c;
-#if S3R_FASTDIV
-    if (div_in_range(w0, ooz) & div_in_range(w1, ooz) & div_in_range(w2, ooz)) {
+    if (kFast && (div_in_range(w0, ooz) & div_in_range(w1, ooz) & div_in_range(w2, ooz))) {
         const float r = div_recip(ooz);
         a = div_with_recip(w0, ooz, r); b = div_with_recip(w1, ooz, r); c = div_with_recip(w2, ooz, r);
-    } else
-#endif
-    {
+    } else {
         a = w0 / ooz; b = w1 / ooz; c = w2 / ooz;
     }
     const F3 P = mk3((c0.x * a + c1.x * b) + c2.x * c, (c0.y * a + c1.y * b) + c2.y * c,
                      (c0.z * a + c1.z * b) + c2.z * c);
-    const F3 pn = S3R_NORMALIZE(P);
+    auto norm = [](F3 v) { return kFast ? fast_normalize3_dev(v) : fast_normalize3(v); };
+    const F3 pn = norm(P);
     const F3 point = mk3(-pn.x, -pn.y, -pn.z);
     const F3 N = mk3((n0.x * a + n1.x * b) + n2.x * c, (n0.y * a + n1.y * b) + n2.y * c,
                      (n0.z * a + n1.z * b) + n2.z * c);
-    const F3 normal = S3R_NORMALIZE(N);
-    const F3 halfway = S3R_NORMALIZE(add3(point, normal));
+    const F3 normal = norm(N);
+    const F3 halfway = norm(add3(point, normal));
     const float s = dot3(halfway, normal);
     F3 col;
     if (kind == kColour) {
@@ -605,13 +603,10 @@ S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float
         const float mv = (k0.y * a + k0.w * b) + k1.y * c;
         const float dvx = fabsf(k2.x - mu * k1.z), dvy = fabsf(k2.y - mv * k1.w);
         float lvx, lvy;
-#if S3R_FASTDIV
-        if (div_in_range(ooz, dvx) & div_in_range(ooz, dvy)) {
+        if (kFast && (div_in_range(ooz, dvx) & div_in_range(ooz, dvy))) {
             lvx = div_with_recip(ooz, dvx, div_recip(dvx));
             lvy = div_with_recip(ooz, dvy, div_recip(dvy));
-        } else
-#endif
-        {
+        } else {
             lvx = ooz / dvx;
             lvy = ooz / dvy;
         }
@@ -636,7 +631,10 @@ S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float
 S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0,
                                     float4 k1, float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1,
                                     float w2, float ooz, const uint32_t *__restrict__ tex, uint32_t ntex) {
-    bool ok = div_in_range(w0, ooz) & div_in_range(w1, ooz) & div_in_range(w2, ooz);
+    // operand ranges: w, 1/z and the texture derivatives in [2^-40, 2^20) -- biased exponents in
+    // [87, 146], so every quotient below meets div_in_range (NaN fails the compares)
+    auto inr = [](float x) { return (fabsf(x) >= 0x1p-40f) & (fabsf(x) < 0x1p20f); };
+    bool ok = inr(w0) & inr(w1) & inr(w2) & inr(ooz);
     const float r = div_recip(ooz);
     const float a = div_with_recip(w0, ooz, r), b = div_with_recip(w1, ooz, r), c = div_with_recip(w2, ooz, r);
     // texture coordinates first: the texel load overlaps the normalisations
@@ -644,7 +642,7 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     const float mv = (k0.y * a + k0.w * b) + k1.y * c;
     const float dvx = fabsf(k2.x - mu * k1.z), dvy = fabsf(k2.y - mv * k1.w);
     const bool texd = kind != kColour;
-    ok &= !texd | (div_in_range(ooz, dvx) & div_in_range(ooz, dvy));
+    ok &= !texd | (inr(dvx) & inr(dvy));
     const float lvx = div_with_recip(ooz, dvx, div_recip(dvx));
     const float lvy = div_with_recip(ooz, dvy, div_recip(dvy));
 #if S3R_TEX_EARLY
@@ -673,7 +671,11 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
                         : mk3((k0.x * a + k1.x * b) + k2.x * c, (k0.y * a + k1.y * b) + k2.y * c,
                               (k0.z * a + k1.z * b) + k2.z * c);
     uint32_t res = rgb_pack(s * col.x, s * col.y, s * col.z);
-    if (!ok) res = shade_core(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, w0, w1, w2, ooz, tex, ntex);
+    if (!ok) {
+        // opaque copies: keeps the compiler from speculating the fallback's divisions into the fast path
+        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(ooz));
+        res = shade_core<false>(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, w0, w1, w2, ooz, tex, ntex);
+    }
     return res;
 }
 
