@@ -883,6 +883,15 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         if (lane == 0) sh.cnt = cnt;
     }
     __syncthreads();
+    // batch 0's walk state, fetched speculatively with the raster constants: the start-table index
+    // is 0 (at xmin) or 1 + xs / kStartPx (start_index), so both candidates are read now and the
+    // entry's xmin picks one after load_entries (one dependent round trip less per workgroup)
+    float spec0 = 0.0f, spec1 = 0.0f;
+    if (sh.cnt <= kListMax && row_ok && lane < 63 && tl < sh.cnt) {
+        const size_t sb = ((size_t)sh.ent[tl].slot * rows_local + lr) * nst;
+        spec0 = rowtab[sb * 4 + comp];
+        spec1 = rowtab[(sb + 1u + xs / kStartPx) * 4 + comp];
+    }
     if (sh.cnt <= kListMax) {
         load_entries(tris, sh, sh.cnt, wave, lane);
         overflow = false;
@@ -907,7 +916,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                 if (y >= e.ymin && y <= e.ymax) {
                     uint32_t k;
                     const uint32_t j = start_index(e.xmin, xs, &k);
-                    st_c[b * 64 + lane] = rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
+                    st_c[b * 64 + lane] = b == 0 ? (j == 0 ? spec0 : spec1)
+                                                 : rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
                     st_k[b * 64 + lane] = k;
                 }
             }
