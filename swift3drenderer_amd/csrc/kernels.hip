@@ -330,6 +330,8 @@ struct alignas(16) Entry {              // 48 B per listed triangle (LDS, shared
 struct FragShared {
     Entry ent[kListMax];
     uint32_t cnt, next;
+    uint32_t *cost_dst;                  // order_bins cost of this bin (null: no order), and
+    uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits)
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
     float tab[kWaves][kTables][kChunk];  // exact S(c, d, k), k < kChunk, filled by sequential adds
@@ -449,6 +451,36 @@ __device__ __forceinline__ uint32_t start_index(uint32_t xmin, uint32_t xs, uint
 S3R_HD uint32_t start_entries_of(uint32_t W) { return (W + kStartPx - 1) / kStartPx + 1u; }
 uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
 
+// Longest-first order of the fragment bins (workgroups): a fragment launch is several rounds of
+// resident workgroups whose costs differ ~8x (textured floor rows vs sky), and the launch order
+// (top-down) can leave the costliest rows for the last round.  One workgroup counting-sorts the bins
+// by their cost when the buffer set was last used (k_fragment's order[n + bin], 10 ns ticks; stale
+// values from another frame size are only hints) into kOrderBuckets buckets, costliest first; perm
+// is always a permutation of [0, n).
+constexpr uint32_t kOrderBuckets = 32;
+__device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32_t *__restrict__ perm) {
+    __shared__ uint32_t hist[kOrderBuckets];
+    __shared__ uint32_t cmax;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if (tid < kOrderBuckets) hist[tid] = 0;
+    if (tid == 0) cmax = 1;
+    __syncthreads();
+    uint32_t m = 1;
+    for (uint32_t i = tid; i < n; i += nt) m = max(m, cost[i]);
+    atomicMax(&cmax, m);
+    __syncthreads();
+    const uint64_t mx = (uint64_t)cmax + 1u;
+    auto bucket = [&](uint32_t c) { return (uint32_t)min((uint64_t)c * kOrderBuckets / mx, (uint64_t)kOrderBuckets - 1u); };
+    for (uint32_t i = tid; i < n; i += nt) atomicAdd(&hist[bucket(cost[i])], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int b = (int)kOrderBuckets - 1; b >= 0; b--) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += nt) perm[atomicAdd(&hist[bucket(cost[i])], 1u)] = i;
+}
+
 // ------------------------------------------------------------------ K1: geometry, one launch
 // Per frame, on the geometry stream (overlapping the previous frame's fragment kernel): one
 // workgroup per (slot, block of kGeoRows local rows) x 3 components.
@@ -470,9 +502,14 @@ __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
     const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, uint32_t nwords, TriSetup *__restrict__ tris,
-    float *__restrict__ rowtab, unsigned long long *__restrict__ binmask, uint32_t tag) {
+    float *__restrict__ rowtab, unsigned long long *__restrict__ binmask, uint32_t tag,
+    uint32_t nbins, uint32_t *__restrict__ order) {
     __shared__ TriSetup sts;
     const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
+    if (slot >= 2u * ntri) {                   // the extra column: this frame's fragment order
+        if (rb == 0) order_bins(order + nbins, nbins, order);
+        return;
+    }
 #ifdef S3R_STATS
     const unsigned long long t_start = wall_clock64();
     if (tid == 0) atomicMin(&g_tstats[2], t_start);
@@ -823,7 +860,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   uint32_t rows_local,
                                                   const unsigned long long *__restrict__ binmask,
                                                   uint32_t nwords, uint32_t done_tag, uint32_t *done_flag,
-                                                  uint32_t prev_tag) {
+                                                  uint32_t prev_tag, uint32_t *__restrict__ order) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -832,7 +869,14 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     if (done_flag && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(done_flag, prev_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t bid = blockIdx.x;
+    // longest-first workgroup order (order = [perm | cost] of this buffer set, order_bins in
+    // k_geometry) or the launch order; either way a permutation of the bins, so the pixels do not
+    // depend on it
+    const uint32_t bid = order ? order[blockIdx.x] : blockIdx.x;
+    if (threadIdx.x == 0) {              // kept in LDS: no registers live across the kernel
+        sh.cost_dst = order ? order + gridDim.x + bid : nullptr;
+        sh.t_start = (uint32_t)wall_clock64();
+    }
     const uint32_t blk = bid / segs, seg = bid - blk * segs;
     const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
@@ -1107,6 +1151,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         S3R_WGC_ADD(2);
     }
     S3R_WGT(3);
+    // this bin's cost (wave 0's wall time, 10 ns ticks) for the buffer set's next order_bins
+    if (threadIdx.x == 0 && sh.cost_dst) *sh.cost_dst = (uint32_t)wall_clock64() - sh.t_start;
     S3R_WGC_STORE(n0);
 #ifdef S3R_STATS
     {
@@ -1817,22 +1863,23 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done) {
+                     hipEvent_t done, uint32_t *order) {
     if (ntri == 0 || rows_local == 0) {
         if (done) (void)hipEventRecord(done, st);
         return;
     }
     // the completion event is recorded by the launch itself (one host call instead of two)
-    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri, (rows_local + kGeoRows - 1) / kGeoRows), dim3(3 * kGeoRows), 0,
-                          st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band, nparts,
-                          part, rows_local, fragment_segments(W), kChunk * g_segch, bin_words(2 * ntri), tris, rowtab,
-                          binmask, tag);
+    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri + (order ? 1u : 0u), (rows_local + kGeoRows - 1) / kGeoRows),
+                          dim3(3 * kGeoRows), 0, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor,
+                          W, H, band, nparts, part, rows_local, fragment_segments(W), kChunk * g_segch,
+                          bin_words(2 * ntri), tris, rowtab, binmask, tag, (uint32_t)fragment_bins(W, rows_local),
+                          order);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, const unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag) {
+                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -1843,11 +1890,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binmask,
-                              bin_words(nslots), tag, done_flag, prev_tag);
+                              bin_words(nslots), tag, done_flag, prev_tag, order);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots), tag, done_flag,
-                           prev_tag);
+                           prev_tag, order);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

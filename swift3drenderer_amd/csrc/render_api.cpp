@@ -42,6 +42,7 @@ struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
 // geometry of two consecutive frames and the previous frame's fragment kernel can all overlap.
 constexpr int kSets = 4;
 constexpr int kGeoStreams = 2;
+constexpr uint64_t kLptMinBins = 8000;      // longest-first fragment order from this many bins (see render_core)
 
 struct Lib {
     bool initialized = false;
@@ -69,6 +70,9 @@ struct Lib {
     size_t rowtab_cap = 0;
     unsigned long long *binmask[kSets] = {}; // per fragment workgroup: tagged slot-mask words
     uint64_t binmask_cap = 0;
+    // longest-first fragment order, per buffer set: [perm | cost] (s3r_kernels.h launch_fragment)
+    uint32_t *order[kSets] = {};
+    uint64_t order_cap = 0;
     // tile path (many triangles): per-tile counts, offsets, scatter cursors, slot lists
     uint32_t *tile_counts[kSets] = {}, *tile_offs[kSets] = {};
     uint32_t *tile_cursor[kSets] = {}, *tile_total[kSets] = {};
@@ -315,7 +319,7 @@ void release_all() {
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
         for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
-            void *set[] = {g.tris[q], g.rowtab[q], g.binmask[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
+            void *set[] = {g.tris[q], g.rowtab[q], g.binmask[q], g.order[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
                            g.tile_list[q], g.recs[q], g.boxes[q], g.app_list[q], g.app_count[q]};
             for (void *p : set)
                 if (p) (void)hipFree(p);
@@ -528,6 +532,20 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
         }
         g.binmask_cap = nmask;
     }
+    // longest-first order only where a launch is several rounds of resident workgroups (~1 280 on
+    // the chip): a frame part of one round gains nothing and would pay the order column's time
+    const uint64_t bins = fragment_bins(W, rows_local);
+    const char *lpt_env = getenv("S3R_LPT_MIN");            // tuning / test override
+    const bool lpt = g.ntri > 0 && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins);
+    if (lpt && g.order_cap < bins) {
+        HIPCHECK(hipDeviceSynchronize());
+        for (int q = 0; q < kSets; q++) {
+            if (g.order[q]) HIPCHECK(hipFree(g.order[q]));
+            g.order[q] = dalloc<uint32_t>(2 * bins);
+            HIPCHECK(hipMemset(g.order[q], 0, 2 * bins * sizeof(uint32_t)));
+        }
+        g.order_cap = bins;
+    }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
     const uint32_t p = next_set();
     hipStream_t geo = g.geo[g.frame_no % kGeoStreams];
@@ -543,7 +561,8 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     hp.lap(2);
     const uint32_t tag = g.frame_no;              // >= 1: frame k's tag for its slot masks and completion
     launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], tag, geo, g.geo_done[p]);
+                    rows_local, g.tris[p], g.rowtab[p], g.binmask[p], tag, geo, g.geo_done[p],
+                    lpt ? g.order[p] : nullptr);
     hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
@@ -553,7 +572,8 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.binmask[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag);
+                    g.binmask[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag,
+                    lpt ? g.order[p] : nullptr);
     g.issued_tag[p] = tag;
     g.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));

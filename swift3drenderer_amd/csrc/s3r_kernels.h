@@ -5,13 +5,17 @@
 namespace s3r {
 
 // `done` (may be null): recorded on `st` when the launched kernel completes.
+// order (may be null: launch order): 2 x fragment_bins() words, [perm | cost] -- launch_geometry's
+// extra workgroup (order non-null there) writes perm, the launch's workgroup -> bin map, from the
+// costs; the fragment launch reads perm and stores each bin's time into cost, for the next frame
+// on the same buffer set (a hint only: any permutation renders the same pixels).
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, const unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag);
+                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their slot masks:
 // fragment_bins() masks of bin_words(nslots) tagged words each: (frame tag << 32) | 32 slot bits, a
@@ -28,7 +32,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done);
+                     hipEvent_t done, uint32_t *order);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();

@@ -226,3 +226,35 @@ def test_small_parts_overflow(gpu_renderer, tmp_path):
     path = str(tmp_path / 'stack-small.bin')
     stacked_quads_scene(path, size=0.08)
     _parts_vs_oracle(gpu_renderer, path, [(0, 0, 0, 0, 0, 0)], 3840, 2160, 8, 16, (0, 5))
+
+
+def test_longest_first_order(gpu_renderer, scene_dir, monkeypatch):
+    """Longest-first fragment order (k_geometry's order column from earlier frames' per-bin costs,
+    render_api.cpp kLptMinBins) forced on for every frame size: held, moving, resized and pipelined
+    frames all equal the oracle's -- the order is a permutation of the bins, never a change of pixels."""
+    import torch
+    from oracle.oracle import OracleRenderer
+    monkeypatch.setenv('S3R_LPT_MIN', '0')
+    path = scene_dir['full']
+    o = OracleRenderer(path)
+    gpu_renderer.configure(path)
+    seq = [(640, 480, (0, 0, 0, 0, 0, -150))] * 3 + [(640, 480, (2, 0, 1, 0, 5, -150)), (320, 240, (0, 0, 0, 0, 0, -150)),
+                                                  (800, 600, (0, 3, 0, 0, -4, -140)), (800, 600, (0, 0, 0, 0, 0, -140))]
+    for k, (w, h, inp) in enumerate(seq):
+        want = o.update_and_render(w, h, inp)
+        got = gpu_renderer.update_and_render(w, h, inp)
+        assert np.array_equal(got, want), f'frame {k} {w}x{h}: ' + diff_report(got, want)
+    W, H = 640, 480
+    inputs = [(0, 0, 0, 0, 3.0 * k, -150 + k) for k in range(10)]
+    wants = [o.update_and_render(W, H, inp) for inp in inputs]
+    st = torch.cuda.Stream()
+    bufs = []
+    for inp in inputs:                      # back to back: several frames in flight
+        buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
+        with torch.cuda.stream(st):
+            gpu_renderer.render_bands(inp, W, H, H, 1, 0, buf.data_ptr(), st.cuda_stream)
+        bufs.append(buf)
+    torch.cuda.synchronize()
+    for k, buf in enumerate(bufs):
+        got = buf.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, wants[k]), f'pipelined frame {k}: ' + diff_report(got, wants[k])
