@@ -494,7 +494,10 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
 //     boundary inside the bbox (:374), storing the row start and each segment start.
 // rowtab[((slot * rows_local + lr) * nst + j) * 4 + c], nst = start_entries(W): j = 0 at x = xmin,
 // j = 1 + j' at x = j' * kStartPx (only boundaries in (xmin, xmax] are written).
-constexpr uint32_t kGeoRows = 128;
+#ifndef S3R_GEO_ROWS
+#define S3R_GEO_ROWS 128
+#endif
+constexpr uint32_t kGeoRows = S3R_GEO_ROWS;
 static_assert(kGeoRows % kWaves == 0, "geometry row blocks hold whole fragment row blocks");
 
 __global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
