@@ -330,11 +330,10 @@ struct alignas(16) Entry {              // 48 B per listed triangle (LDS, shared
 struct FragShared {
     Entry ent[kListMax];
     uint32_t cnt, next;
-    uint32_t *cost_dst;                  // order_bins cost of this bin (null: no order), and
-    uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits)
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
     float tab[kWaves][kTables][kChunk];  // exact S(c, d, k), k < kChunk, filled by sequential adds
+    uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
 };
 constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
@@ -455,30 +454,50 @@ uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
 // resident workgroups whose costs differ ~8x (textured floor rows vs sky), and the launch order
 // (top-down) can leave the costliest rows for the last round.  One workgroup counting-sorts the bins
 // by their cost when the buffer set was last used (k_fragment's order[n + bin], 10 ns ticks; stale
-// values from another frame size are only hints) into kOrderBuckets buckets, costliest first; perm
-// is always a permutation of [0, n).
+// values from another frame size are only hints; no fragment launch of the set runs meanwhile, so
+// both passes read the same values) into kOrderBuckets quarter-octave buckets,
+// costliest first; perm is always a permutation of [0, n).
 constexpr uint32_t kOrderBuckets = 32;
+// bucket of a cost: a quarter octave each from 2^6 ticks (0.64 us) -- no max pass over the costs
+__device__ __forceinline__ uint32_t order_bucket(uint32_t c) {
+    const float l = __log2f((float)max(c, 64u)) * 4.0f - 24.0f;
+    return min((uint32_t)l, kOrderBuckets - 1u);
+}
+// the two passes read kOrderUnroll costs per thread before using them (independent loads in flight)
+constexpr uint32_t kOrderUnroll = 8;
 __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32_t *__restrict__ perm) {
     __shared__ uint32_t hist[kOrderBuckets];
-    __shared__ uint32_t cmax;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if (tid < kOrderBuckets) hist[tid] = 0;
-    if (tid == 0) cmax = 1;
     __syncthreads();
-    uint32_t m = 1;
-    for (uint32_t i = tid; i < n; i += nt) m = max(m, cost[i]);
-    atomicMax(&cmax, m);
-    __syncthreads();
-    const uint64_t mx = (uint64_t)cmax + 1u;
-    auto bucket = [&](uint32_t c) { return (uint32_t)min((uint64_t)c * kOrderBuckets / mx, (uint64_t)kOrderBuckets - 1u); };
-    for (uint32_t i = tid; i < n; i += nt) atomicAdd(&hist[bucket(cost[i])], 1u);
+    for (uint32_t base = 0; base < n; base += kOrderUnroll * nt) {
+        uint32_t b[kOrderUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kOrderUnroll; u++) {
+            const uint32_t i = base + u * nt + tid;
+            b[u] = i < n ? order_bucket(cost[i]) : kOrderBuckets;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrderUnroll; u++)
+            if (b[u] < kOrderBuckets) atomicAdd(&hist[b[u]], 1u);
+    }
     __syncthreads();
     if (tid == 0) {
         uint32_t run = 0;
         for (int b = (int)kOrderBuckets - 1; b >= 0; b--) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += nt) perm[atomicAdd(&hist[bucket(cost[i])], 1u)] = i;
+    for (uint32_t base = 0; base < n; base += kOrderUnroll * nt) {
+        uint32_t b[kOrderUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kOrderUnroll; u++) {
+            const uint32_t i = base + u * nt + tid;
+            b[u] = i < n ? order_bucket(cost[i]) : kOrderBuckets;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrderUnroll; u++)
+            if (b[u] < kOrderBuckets) perm[atomicAdd(&hist[b[u]], 1u)] = base + u * nt + tid;
+    }
 }
 
 // ------------------------------------------------------------------ K1: geometry, one launch
@@ -876,10 +895,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     // k_geometry) or the launch order; either way a permutation of the bins, so the pixels do not
     // depend on it
     const uint32_t bid = order ? order[blockIdx.x] : blockIdx.x;
-    if (threadIdx.x == 0) {              // kept in LDS: no registers live across the kernel
-        sh.cost_dst = order ? order + gridDim.x + bid : nullptr;
-        sh.t_start = (uint32_t)wall_clock64();
-    }
+    if (order && threadIdx.x == 0) sh.t_start = (uint32_t)wall_clock64();   // in LDS: no live registers
     const uint32_t blk = bid / segs, seg = bid - blk * segs;
     const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
@@ -1155,7 +1171,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     }
     S3R_WGT(3);
     // this bin's cost (wave 0's wall time, 10 ns ticks) for the buffer set's next order_bins
-    if (threadIdx.x == 0 && sh.cost_dst) *sh.cost_dst = (uint32_t)wall_clock64() - sh.t_start;
+    if (order && threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
     S3R_WGC_STORE(n0);
 #ifdef S3R_STATS
     {

@@ -104,4 +104,9 @@ def test_gpu_band_parts_reassemble(gpu_renderer, scene_dir, nparts, band):
         parts.append(buf.cpu().numpy()[:rows])
     torch.cuda.synchronize()
     got = assemble(parts, H, band)
-    assert np.array_equal(got, full.cpu().numpy())
+    want = full.cpu().numpy()
+    if not np.array_equal(got, want):
+        ys, xs = np.nonzero(got != want)
+        bad_parts = sorted({(int(y) // band) % nparts for y in ys})
+        raise AssertionError(f'{len(ys)} pixels differ (rows {ys.min()}-{ys.max()}, parts {bad_parts}); first at '
+                             f'(x={xs[0]}, y={ys[0]}): parts {got[ys[0], xs[0]]:#x} whole frame {want[ys[0], xs[0]]:#x}')
