@@ -41,7 +41,10 @@ struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
 // of frame k - kSets (the set's last reader) is done, on geometry stream k % kGeoStreams, so the
 // geometry of two consecutive frames and the previous frame's fragment kernel can all overlap.
 constexpr int kSets = 4;
-constexpr int kGeoStreams = 2;
+#ifndef S3R_GEO_STREAMS
+#define S3R_GEO_STREAMS 2
+#endif
+constexpr int kGeoStreams = S3R_GEO_STREAMS;
 constexpr uint64_t kLptMinBins = 8000;      // longest-first fragment order from this many bins (see render_core)
 
 struct Lib {
