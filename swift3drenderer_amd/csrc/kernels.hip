@@ -519,7 +519,10 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
 constexpr uint32_t kGeoRows = S3R_GEO_ROWS;
 static_assert(kGeoRows % kWaves == 0, "geometry row blocks hold whole fragment row blocks");
 
-__global__ void __launch_bounds__(3 * kGeoRows) k_geometry(
+#ifndef S3R_GEO_OCC
+#define S3R_GEO_OCC 6                  // min waves per SIMD of k_geometry: 80 VGPRs (115 uncapped), see DESIGN
+#endif
+__global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     const float4 *__restrict__ vtx, const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
     const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,

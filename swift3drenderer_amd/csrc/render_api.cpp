@@ -45,7 +45,7 @@ constexpr int kSets = 4;
 #define S3R_GEO_STREAMS 2
 #endif
 constexpr int kGeoStreams = S3R_GEO_STREAMS;
-constexpr uint64_t kLptMinBins = 8000;      // longest-first fragment order from this many bins (see render_core)
+constexpr uint64_t kLptMinBins = 2560;      // longest-first fragment order from this many bins (2 rounds; see render_core)
 
 struct Lib {
     bool initialized = false;
@@ -533,6 +533,9 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
             g.binmask[p] = dalloc<unsigned long long>(nmask);
             HIPCHECK(hipMemset(g.binmask[p], 0, nmask * sizeof(unsigned long long)));   // tag 0: no frame
         }
+        // hipMemset runs on the null stream, which does not order the non-blocking geometry
+        // streams: finish it before the next k_geometry sets bits in these words
+        HIPCHECK(hipDeviceSynchronize());
         g.binmask_cap = nmask;
     }
     // longest-first order only where a launch is several rounds of resident workgroups (~1 280 on
@@ -547,6 +550,7 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
             g.order[q] = dalloc<uint32_t>(2 * bins);
             HIPCHECK(hipMemset(g.order[q], 0, 2 * bins * sizeof(uint32_t)));
         }
+        HIPCHECK(hipDeviceSynchronize());     // (as for the slot masks: before k_geometry writes perm)
         g.order_cap = bins;
     }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
