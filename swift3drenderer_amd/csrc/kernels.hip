@@ -520,7 +520,7 @@ constexpr uint32_t kGeoRows = S3R_GEO_ROWS;
 static_assert(kGeoRows % kWaves == 0, "geometry row blocks hold whole fragment row blocks");
 
 #ifndef S3R_GEO_OCC
-#define S3R_GEO_OCC 6                  // min waves per SIMD of k_geometry: 80 VGPRs (115 uncapped), see DESIGN
+#define S3R_GEO_OCC 5                  // min waves per SIMD of k_geometry: 96 VGPRs (115 uncapped), see DESIGN
 #endif
 __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     const float4 *__restrict__ vtx, const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
