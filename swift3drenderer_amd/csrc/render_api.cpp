@@ -45,7 +45,7 @@ constexpr int kSets = 4;
 #define S3R_GEO_STREAMS 2
 #endif
 constexpr int kGeoStreams = S3R_GEO_STREAMS;
-constexpr uint64_t kLptMinBins = 2560;      // longest-first fragment order from this many bins (2 rounds; see render_core)
+constexpr uint64_t kLptMinBins = 4000;      // longest-first fragment order from this many bins (~3 rounds; see render_core)
 
 struct Lib {
     bool initialized = false;
