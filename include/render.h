@@ -87,7 +87,8 @@ void s3r_timing(int enable);
 void s3r_timing_collect(double out[3]);
 
 /* Scene counts after init: out = {vertices, indices, attributes, texels, triangle slots,
- * (slot, tile) pairs binned in the last frame (tile path), the last frame's path (1 rows, 2 tiles), 0}. */
+ * (slot, tile) pairs binned in the last frame (tile path), the last frame's path (1 rows, 2 tiles),
+ * host-buffer registrations updateAndRender found stale and replaced}. */
 void s3r_scene_counts(uint64_t out[8]);
 
 /* Copy the current camera matrix (3 rows x 4) and raster factor. */
@@ -117,6 +118,10 @@ int s3r_selftest_walk_device(const float *s, const float *d, const uint32_t *n, 
  * [2^-48, 2^64); 2: `count` hashed in-range quotients; 3: `count` hashed vector normalisations.
  * out = {mismatches, first mismatching index or ~0}; returns 0 when the test ran. */
 int s3r_selftest_fastmath_device(uint32_t mode, uint64_t count, uint64_t out[2]);
+/* Test hook: drain the device and continue the frame count at frame_no (clamped below the point
+ * where the library restarts its uint32 frame tags), so tests reach the restart in a few frames.
+ * No effect before the first frame. */
+void s3r_debug_set_frame_count(uint32_t frame_no);
 
 #ifdef __cplusplus
 }

@@ -100,7 +100,10 @@ struct Lib {
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
+    // the previous frame's stream; NULL is a valid caller stream (the legacy default stream), so
+    // whether a previous frame exists is its own flag
     hipStream_t last_stream = nullptr;
+    bool have_last = false;
     hipEvent_t handoff = nullptr;
     uint32_t frame_no = 0;                     // frames issued: set frame_no % kSets
     uint32_t *frame = nullptr;
@@ -110,6 +113,7 @@ struct Lib {
     // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
     struct Reg { void *p; size_t n; bool ok; };
     std::vector<Reg> regs;
+    uint64_t stale_pins = 0;                   // registrations found stale and replaced (updateAndRender)
 
     bool timing = false;
     std::vector<TimingSlot> tslots;
@@ -378,8 +382,26 @@ TimingSlot *timing_slot() {
     return &g.tslots[g.tcount++];
 }
 
+// Frame tags are the uint32 frame number (0 = none): the slot-mask words' high halves, issued_tag,
+// last_tag and the completion word.  Before the count wraps (~62 h at 19 k fps) every stream is
+// drained, the slot masks are zeroed and the count restarts, so no tag is reused while a word or a
+// completion flag still carries it.
+constexpr uint32_t kTagLimit = 0xFFFFFF00u;
+
+void restart_tags(uint32_t next_frame_no) {
+    HIPCHECK(hipDeviceSynchronize());
+    for (int p = 0; p < kSets; p++)
+        if (g.binmask[p]) HIPCHECK(hipMemset(g.binmask[p], 0, g.binmask_cap * sizeof(unsigned long long)));
+    HIPCHECK(hipDeviceSynchronize());
+    g.frame_no = next_frame_no;
+    for (uint32_t &t : g.issued_tag) t = 0;
+    g.last_tag = 0;
+    if (g.done_host) __atomic_store_n(g.done_host, 0u, __ATOMIC_RELEASE);
+}
+
 // The buffer set of the frame being issued; frames cycle through kSets sets.
 uint32_t next_set() {
+    if (g.frame_no >= kTagLimit) restart_tags(0);
     g.frame_no++;
     return g.frame_no % kSets;
 }
@@ -412,11 +434,14 @@ void wait_set_free(uint32_t p) {
 // previous one, that stream first waits for the previous frame's fragment stage (one event): the
 // row path's completion chain (wait_set_free) and the tile path's shared key buffer assume it.
 void follow_previous_frame(hipStream_t st) {
-    if (g.last_stream && st != g.last_stream) {
+    // the null stream does not order our non-blocking streams (nor they it): a switch from or to
+    // NULL needs the event like any other
+    if (g.have_last && st != g.last_stream) {
         HIPCHECK(hipEventRecord(g.handoff, g.last_stream));
         HIPCHECK(hipStreamWaitEvent(st, g.handoff, 0));
     }
     g.last_stream = st;
+    g.have_last = true;
 }
 
 // S3R_SERIAL (profiling): the geometry waits for every earlier fragment kernel -- no overlap.
@@ -600,6 +625,37 @@ bool host_pinned(void *p, size_t n) {
     return ok;
 }
 
+void drop_registration(void *p, size_t n) {
+    for (size_t i = 0; i < g.regs.size(); i++) {
+        if (g.regs[i].p == p && g.regs[i].n == n) {
+            if (g.regs[i].ok) (void)hipHostUnregister(p);
+            g.regs.erase(g.regs.begin() + (long)i);
+            return;
+        }
+    }
+}
+
+// A cached registration is keyed by (pointer, size).  If the caller freed its buffer and got a new
+// one at the same address, a registration that still pins the old pages would take the frame.
+// Pixels are 0x00RRGGBB, so a word with a set high byte is never a pixel: such a sentinel is stored
+// through the caller's pointer at the buffer's ends and every 64 KiB before the copy; if one
+// survives the copy, the copy did not reach the caller's pages and is redone through a new
+// registration.
+constexpr uint32_t kStaleProbe = 0xFF5A5A5Au;
+constexpr size_t kProbeStride = 16384;        // words: 64 KiB
+
+void stamp_probes(uint32_t *buf, size_t words) {
+    for (size_t i = 0; i < words; i += kProbeStride) buf[i] = kStaleProbe;
+    buf[words - 1] = kStaleProbe;
+}
+
+bool probes_overwritten(const uint32_t *buf, size_t words) {
+    const volatile uint32_t *b = buf;
+    for (size_t i = 0; i < words; i += kProbeStride)
+        if (b[i] == kStaleProbe) return false;
+    return b[words - 1] != kStaleProbe;
+}
+
 }  // namespace
 
 extern "C" {
@@ -617,12 +673,23 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     // memset_pattern4 fills bufferSize bytes (render.cpp:282); the frame covers W*H pixels.
     const size_t frame_bytes = npx * 4;
     const size_t copy_bytes = pixel_data->bufferSize < frame_bytes ? pixel_data->bufferSize : frame_bytes;
+    const size_t copy_words = copy_bytes / 4;
+    bool pinned = false;
     if (copy_bytes) {
-        host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        if (pinned && copy_words) stamp_probes(pixel_data->buffer, copy_words);
         HIPCHECK(hipMemcpyAsync(pixel_data->buffer, g.frame, copy_bytes, hipMemcpyDeviceToHost, g.stream));
     }
     for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
     HIPCHECK(hipStreamSynchronize(g.stream));
+    if (pinned && copy_words && !probes_overwritten(pixel_data->buffer, copy_words)) {
+        // a stale registration (buffer freed and reallocated at the same address): pin anew, copy again
+        drop_registration(pixel_data->buffer, pixel_data->bufferSize);
+        g.stale_pins++;
+        host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        HIPCHECK(hipMemcpyAsync(pixel_data->buffer, g.frame, copy_bytes, hipMemcpyDeviceToHost, g.stream));
+        HIPCHECK(hipStreamSynchronize(g.stream));
+    }
 }
 
 __attribute__((visibility("default"))) int s3r_configure(const char *data_path, int device) {
@@ -670,6 +737,14 @@ __attribute__((visibility("default"))) int64_t s3r_render_bands(const Input *inp
     return rows;
 }
 
+// Test hook: drain the device and continue the frame count at `frame_no` (tags above every tag in use
+// keep the slot masks valid), to exercise the tag restart before the uint32 count wraps.
+__attribute__((visibility("default"))) void s3r_debug_set_frame_count(uint32_t frame_no) {
+    if (!g.initialized) return;
+    HIPCHECK(hipSetDevice(g.device));
+    restart_tags(frame_no > kTagLimit ? kTagLimit : frame_no);
+}
+
 __attribute__((visibility("default"))) void s3r_timing(int enable) {
     g.timing = enable != 0;
     g.tcount = 0;
@@ -695,7 +770,7 @@ __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
     out[0] = g.nv; out[1] = g.nindices; out[2] = g.na; out[3] = g.ntex; out[4] = 2ull * g.ntri;
     out[5] = g.last_pairs;                   // tile path: (slot, tile) pairs binned last frame
     out[6] = (uint64_t)g.last_path;          // fragment stage of the last frame: 1 rows, 2 tiles
-    out[7] = 0;
+    out[7] = g.stale_pins;                   // stale host registrations replaced by updateAndRender
 }
 
 __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {

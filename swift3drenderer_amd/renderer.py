@@ -51,6 +51,8 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double)]
     lib.s3r_scene_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_camera.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.s3r_debug_set_frame_count.argtypes = [ctypes.c_uint32]
+    lib.s3r_debug_set_frame_count.restype = None
     _lib = lib
     return lib
 
@@ -130,6 +132,10 @@ class Renderer:
         f = ctypes.c_float()
         self.lib.s3r_camera(m, ctypes.byref(f))
         return np.array(m, dtype=np.float32).reshape(3, 4), f.value
+
+    def debug_set_frame_count(self, frame_no: int):
+        """Test hook: continue the frame count (the frames' uint32 tags) at frame_no."""
+        self.lib.s3r_debug_set_frame_count(frame_no)
 
     def shutdown(self):
         self.lib.s3r_shutdown()

@@ -1,0 +1,142 @@
+"""Frame ordering and buffer life cycle in the C-ABI shim (render_api.cpp), checked against the oracle.
+
+* frames alternating between the null (legacy default) stream, a side stream and updateAndRender's
+  own stream are ordered (follow_previous_frame: a switch from or to NULL needs the hand-off event);
+* the slot-mask / order buffers regrow between two frames issued back to back without a sync;
+* the uint32 frame tags restart before they wrap (restart_tags);
+* a host buffer freed and reallocated at the same address still receives the frame.
+"""
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleRenderer
+from swift3drenderer_amd import poses
+
+from test_gpu_parity import diff_report
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(n, seed, mouse0=(0.0, -120.0)):
+    rng = np.random.default_rng(seed)
+    mouse = np.array(mouse0, dtype=np.float64)
+    out = []
+    for _ in range(n):
+        keys = rng.integers(0, 2, 4) * rng.uniform(0, 6, 4)
+        mouse += rng.normal(0, 10, 2)
+        out.append((*keys, *mouse))
+    return out
+
+
+@pytest.mark.parametrize('path', ['rows', 'tiles'])
+def test_null_stream_then_side_stream(gpu_renderer, scene_dir, path):
+    """render_bands(stream=0) -> render_bands(side stream) -> updateAndRender -> stream 0 again,
+    issued back to back: every frame equals the oracle's frame for the same inputs."""
+    import torch
+    r = gpu_renderer
+    W, H = 320, 240
+    o = OracleRenderer(scene_dir['full'])
+    r.configure(scene_dir['full'])
+    r.set_raster_path(path)
+    try:
+        inputs = _inputs(14, 5)
+        wants = [o.update_and_render(W, H, inp) for inp in inputs]
+        side = torch.cuda.Stream()
+        plan = ['null', 'null', 'side', 'side', 'null', 'host', 'null', 'side', 'null', 'side', 'side', 'null',
+                'host', 'side']
+        bufs = []
+        for k, (inp, where) in enumerate(zip(inputs, plan)):
+            if where == 'host':
+                got = r.update_and_render(W, H, inp)
+                assert np.array_equal(got, wants[k]), f'{path} frame {k} (updateAndRender): ' + diff_report(got, wants[k])
+                continue
+            buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
+            # no torch work on these streams: the library orders the frames itself
+            r.render_bands(inp, W, H, H, 1, 0, buf.data_ptr(), side.cuda_stream if where == 'side' else 0)
+            bufs.append((k, buf))
+        torch.cuda.synchronize()
+        for k, buf in bufs:
+            got = buf.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, wants[k]), f'{path} frame {k} ({plan[k]}): ' + diff_report(got, wants[k])
+    finally:
+        r.set_raster_path('auto')
+
+
+@pytest.mark.parametrize('path', ['rows', 'tiles'])
+def test_regrow_back_to_back(gpu_renderer, scene_dir, monkeypatch, path):
+    """A small frame, then larger ones issued immediately on the same side stream: the slot masks, the
+    longest-first order buffers (forced on) and the tile buffers are reallocated between frames in
+    flight; the first frame after each regrow equals the oracle's."""
+    import torch
+    monkeypatch.setenv('S3R_LPT_MIN', '0')
+    r = gpu_renderer
+    o = OracleRenderer(scene_dir['full'])
+    r.configure(scene_dir['full'])
+    r.set_raster_path(path)
+    try:
+        sizes = [(160, 120), (1920, 1080), (200, 150), (2560, 1440), (3840, 2160)]
+        inputs = _inputs(len(sizes), 9)
+        wants = [o.update_and_render(w, h, inp) for (w, h), inp in zip(sizes, inputs)]
+        st = torch.cuda.Stream()
+        bufs = []
+        for (w, h), inp in zip(sizes, inputs):
+            buf = torch.empty((h, w), dtype=torch.int32, device='cuda')
+            r.render_bands(inp, w, h, h, 1, 0, buf.data_ptr(), st.cuda_stream)
+            bufs.append(buf)
+        torch.cuda.synchronize()
+        for k, buf in enumerate(bufs):
+            got = buf.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, wants[k]), f'{path} frame {k} {sizes[k]}: ' + diff_report(got, wants[k])
+    finally:
+        r.set_raster_path('auto')
+
+
+def test_frame_tags_restart_before_wrap(gpu_renderer, scene_dir):
+    """Frames issued back to back across the tag restart (the uint32 frame count continued just below
+    the restart point): every frame equals the oracle's, before and after the restart."""
+    import torch
+    r = gpu_renderer
+    W, H = 320, 240
+    o = OracleRenderer(scene_dir['full'])
+    r.configure(scene_dir['full'])
+    script = poses.script('P_over')
+    for t in script:
+        o.update_and_render(W, H, t)
+        r.update_and_render(W, H, t)
+    r.debug_set_frame_count(0xFFFFFF00 - 6)
+    inputs = _inputs(16, 13, mouse0=script[-1][4:6])
+    wants = [o.update_and_render(W, H, inp) for inp in inputs]
+    st = torch.cuda.Stream()
+    bufs = []
+    for inp in inputs:
+        buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
+        r.render_bands(inp, W, H, H, 1, 0, buf.data_ptr(), st.cuda_stream)
+        bufs.append(buf)
+    torch.cuda.synchronize()
+    for k, buf in enumerate(bufs):
+        got = buf.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, wants[k]), f'frame {k} around the tag restart: ' + diff_report(got, wants[k])
+
+
+def test_host_buffer_reallocated_at_same_address(gpu_renderer, scene_dir):
+    """updateAndRender into a caller buffer, which is then freed and replaced by a new buffer of the
+    same size (usually at the same address): the new buffer receives the next frame."""
+    r = gpu_renderer
+    W, H = 1280, 720
+    o = OracleRenderer(scene_dir['full'])
+    r.configure(scene_dir['full'])
+    inputs = _inputs(6, 17)
+    same = 0
+    buf = np.empty((H, W), dtype=np.uint32)
+    for k, inp in enumerate(inputs):
+        want = o.update_and_render(W, H, inp)
+        if k:
+            addr = buf.ctypes.data
+            del buf
+            buf = np.empty((H, W), dtype=np.uint32)
+            buf[:] = 0xABCDEF
+            same += buf.ctypes.data == addr
+        r.update_and_render(W, H, inp, buf)
+        assert np.array_equal(buf, want), f'frame {k}: ' + diff_report(buf, want)
+    print(f'reallocated at the same address {same} of {len(inputs) - 1} times; '
+          f'stale registrations replaced: {r.scene_counts()[7]}')
