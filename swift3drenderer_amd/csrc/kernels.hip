@@ -329,12 +329,13 @@ struct alignas(16) Entry {              // 48 B per listed triangle (LDS, shared
 
 struct FragShared {
     Entry ent[kListMax];
-    uint32_t cnt, next;
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
-    float tab[kWaves][kTables][kChunk];  // exact S(c, d, k), k < kChunk, filled by sequential adds
+    float4 tab4[kWaves][kTables][kChunk / 4];  // exact S(c, d, k), k < kChunk, filled by sequential adds
+    uint32_t cnt, next;
     uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
 };
+static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
 constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask, uint32_t lane) {
@@ -784,18 +785,32 @@ __device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32
     bm.negm = __ballot(v.neg);
     bm.twom = __ballot(v.ov && v.two);
     bm.irrm = __ballot(v.ov && !v.lin && !v.two && !((bm.negm >> (3u * tl)) & 7ull));
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 2048)
+    if (false) {                              // ablation: no tables, no pruning walks
+#else
     if (v.ov && !v.lin && !v.two) {
+#endif
         if ((bm.negm >> (3u * tl)) & 7ull) {
             last = v.c;                       // pruned: keep the state at the chunk start
             v.m = 1u;
         } else {
             const uint32_t r = lane_prefix(bm.irrm, lane);
             if (r < kTables) {
+                // the reference's own sequential adds (render.cpp:374), all kChunk of them, unrolled
+                // and stored four at a time (entries past m are never read); `last` = entry m - 1
                 float w = v.c;
-                float *tb = tab[r];
-                tb[0] = w;
-                for (uint32_t k = 1; k < v.m; k++) { w = w + v.d; tb[k] = w; }
-                last = w;
+                float4 *tb4 = reinterpret_cast<float4 *>(tab[r]);
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 8192)
+                tb4[0] = make_float4(w, w, w, w);     // ablation: no sequential fill
+#else
+#pragma unroll
+                for (uint32_t k4 = 0; k4 < kChunk / 4u; k4++) {
+                    const float a1 = w + v.d, a2 = a1 + v.d, a3 = a2 + v.d;
+                    tb4[k4] = make_float4(w, a1, a2, a3);
+                    w = a3 + v.d;
+                }
+#endif
+                last = tab[r][v.m - 1u];
                 bm.tix = r;
             } else {
                 last = walk(v.c, v.d, v.m - 1u S3R_IT(p_chunk));
@@ -1035,7 +1050,12 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                 v.k0 = max(cx0, r0_xmin);
                 const uint32_t kend = min(cx1, r0_xmax);
                 v.m = kend - v.k0 + 1u;
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 1024)
+                if (true) {                          // ablation: every chunk inside the linear run
+                    if (r0_end == 0u) { r0_base = r0_sc; r0_k = r0_sk; r0_del = r0_d; r0_end = 0xFFFFFFFFu; }
+#else
                 if (v.k0 >= r0_k && kend <= r0_end) {
+#endif
                     // inside the current linear run: exact c + k*delta, no walking, no test
                     v.c = r0_base + (float)(v.k0 - r0_k) * r0_del;
                     v.del = r0_del;
@@ -1061,7 +1081,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                         }
                     }
                     v.lin = j >= (float)(v.m - 1u);
-#if S3R_TWO_PIECE
+#if S3R_TWO_PIECE && !(defined(S3R_ABLATE) && (S3R_ABLATE & 4096))
                     if (!v.lin) {
                         // a binade edge inside the chunk: pixels 0..j are c + k*delta (exact), pixel
                         // j + 1 is the reference's one add across the edge, and from there the next
@@ -1083,7 +1103,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
             }
             BatchMasks bm;
             float last;
-            batch_resolve(v, tl, lane, sh.tab[wave], bm, last S3R_IT(p_chunk));
+            batch_resolve(v, tl, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), bm, last S3R_IT(p_chunk));
             if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
             S3R_WGN(1, bm.irrm ? 1u : 0u);
             S3R_WGN(2, (uint32_t)__builtin_popcountll(bm.ovm & ~(bm.negm | (bm.negm >> 1) | (bm.negm >> 2)) & 0x9249249249249249ull));
@@ -1095,7 +1115,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 4)
                 if (x == 0xFFFFFFFFu) win[0] = (int)(bm.ovm ^ bm.negm);   // keep the phase alive, skip pixels
 #else
-                pixel_phase(v, bm, x, sh.tab[wave], depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
+                pixel_phase(v, bm, x, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
 #endif
             }
         }
@@ -1140,14 +1160,14 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                 }
                 BatchMasks bm;
                 float last;
-                batch_resolve(v, tl, lane, sh.tab[wave], bm, last S3R_IT(p_chunk));
+                batch_resolve(v, tl, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), bm, last S3R_IT(p_chunk));
                 if (v.ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = v.k0 + v.m - 1u; }
                 if (bm.ovm == 0) continue;
 #ifdef S3R_STATS
                 st_batches++;
                 st_irr += (v.ov && !v.lin) ? 1u : 0u;
 #endif
-                pixel_phase(v, bm, x, sh.tab[wave], depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
+                pixel_phase(v, bm, x, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
             }
             if (!overflow || cursor >= nslots) break;
         }
