@@ -964,6 +964,24 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         if (lane == 0) sh.cnt = cnt;
     }
     __syncthreads();
+    if (sh.cnt == 0) {
+        // no triangle meets this block (sky): background only (render.cpp:282), 16 B per lane where
+        // the row segment is 16-B aligned
+        if (row_ok) {
+            uint32_t *seg = out + (size_t)lr * W + xs;
+            const uint32_t n = xe - xs + 1u;
+            if (((size_t)lr * W + xs) % 4u == 0u) {
+                const uint4 bg4 = make_uint4(kBackground, kBackground, kBackground, kBackground);
+                for (uint32_t i = lane; i < n / 4u; i += 64u) reinterpret_cast<uint4 *>(seg)[i] = bg4;
+                for (uint32_t i = (n & ~3u) + lane; i < n; i += 64u) seg[i] = kBackground;
+            } else {
+                for (uint32_t i = lane; i < n; i += 64u) seg[i] = kBackground;
+            }
+        }
+        S3R_WGT(3);
+        if (order && threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
+        return;
+    }
     // batch 0's walk state, fetched speculatively with the raster constants: the start-table index
     // is 0 (at xmin) or 1 + xs / kStartPx (start_index), so both candidates are read now and the
     // entry's xmin picks one after load_entries (one dependent round trip less per workgroup)
