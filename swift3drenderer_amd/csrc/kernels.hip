@@ -298,6 +298,7 @@ constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + co
 #define S3R_WAVES 4
 #endif
 constexpr uint32_t kWaves = S3R_WAVES; // one wave per row: a workgroup is kWaves consecutive local rows
+static_assert(kWaves == 4, "pair records carry the walk state of 4 rows (s3r_kernels.h)");
 constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
 #ifndef S3R_STATE_BATCHES
 #define S3R_STATE_BATCHES 4
@@ -527,8 +528,8 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     const float4 *__restrict__ vtx, const float4 *__restrict__ nrm, const float4 *__restrict__ pay,
     const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-    uint32_t rows_local, uint32_t segs, uint32_t segw, uint32_t nwords, TriSetup *__restrict__ tris,
-    float *__restrict__ rowtab, unsigned long long *__restrict__ binmask, uint32_t tag,
+    uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
+    float *__restrict__ rowtab, unsigned long long *__restrict__ binhdr, uint4 *__restrict__ pairs, uint32_t tag,
     uint32_t nbins, uint32_t *__restrict__ order) {
     __shared__ TriSetup sts;
     const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
@@ -555,8 +556,58 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     if (sts.kind == kDead) { S3R_GWT_END(); return; }
     const uint32_t xmin = sts.xmin, xmax = sts.xmax, ymin = sts.ymin, ymax = sts.ymax;
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
+    const uint32_t nst = start_entries_of(W);
 
-    // bins of this workgroup's rows: (kGeoRows / kWaves) fragment row blocks x segs segments
+    // exact row and start-table points: lane (row, component) walks the reference's sequence exactly
+    // (exact_walk): wy += dy down to its row (render.cpp:378), then w += dx along the row through every
+    // kStartPx boundary inside the bbox (:374)
+    {
+        const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
+        const uint32_t y = row_of(lr);
+        bool walk_row = !(lr >= rows_local || y < ymin || y > ymax || y >= H);
+#if defined(S3R_GEO_ABLATE)                  // 2 = no walks at all
+        if (S3R_GEO_ABLATE & 2) walk_row = false;
+#endif
+        if (walk_row) {
+            float *row = rowtab + ((size_t)slot * rows_local + lr) * nst * 4 + c;
+            const float d = sts.dx[c];
+#ifdef S3R_STATS
+            uint32_t it_row = 0, it_seg = 0;
+            float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin, &it_row);
+#else
+            float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
+#endif
+            row[0] = v;
+            uint32_t xp = xmin;
+#if defined(S3R_GEO_ABLATE)                  // timing-only variants: 1 = no segment starts
+            if (!(S3R_GEO_ABLATE & 1))
+#endif
+            for (uint32_t sg = xmin / kStartPx + 1u; sg + 1u < nst; sg++) {
+                const uint32_t xb = sg * kStartPx;
+                if (xb > xmax) break;
+#ifdef S3R_STATS
+                v = exact_walk(v, d, xb - xp, &it_seg);
+#else
+                v = exact_walk(v, d, xb - xp);
+#endif
+                xp = xb;
+                row[(1 + sg) * 4] = v;
+            }
+#ifdef S3R_STATS
+            atomicAdd(&g_stats[12], (unsigned long long)it_row);
+            atomicMax(&g_stats[13], (unsigned long long)it_row);
+            atomicAdd(&g_stats[14], (unsigned long long)it_seg);
+            atomicMax(&g_stats[15], (unsigned long long)it_seg);
+#endif
+        }
+    }
+    __syncthreads();                           // this workgroup's rowtab rows are written
+    S3R_GWT(2);
+
+    // bins of this workgroup's rows: (kGeoRows / kWaves) fragment row blocks x segs segments.  The
+    // slot takes the next pair of every bin its bbox meets (tagged header: a header still carrying an
+    // older frame's tag counts as empty) and writes its raster constants and the exact walk state of
+    // the bin's rows there (the start-table point of the bin's first pixel, start_index)
     const uint32_t nbr = kGeoRows / kWaves;
     for (uint32_t q = tid; q < nbr * segs; q += 3 * kGeoRows) {
         const uint32_t blk = rb * nbr + q / segs, sg = q % segs;
@@ -568,62 +619,43 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
             y0 = min(y0, yy); y1 = max(y1, yy);
         }
         const uint32_t x0 = sg * segw, x1 = min(W, x0 + segw) - 1u;
-        if (ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)
-        {
-            // tagged word (tag << 32 | bits): a word still carrying an older frame's tag starts empty
-            unsigned long long *w = &binmask[((size_t)blk * segs + sg) * nwords + (slot >> 5)];
-            const unsigned long long tagged = (unsigned long long)tag << 32, bit = 1ull << (slot & 31u);
-            unsigned long long old = *w;
-            for (;;) {
-                const unsigned long long nw = (((old >> 32) == tag) ? old : tagged) | bit;
-                const unsigned long long prev = atomicCAS(w, old, nw);
-                if (prev == old) break;
-                old = prev;
-            }
+        if (!(ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)) continue;
+        const size_t bin = (size_t)blk * segs + sg;
+        unsigned long long *h = &binhdr[bin];
+        unsigned long long old = *h;
+        uint32_t pos;
+        for (;;) {
+            const uint32_t cur = (uint32_t)(old >> 32) == tag ? (uint32_t)old : 0u;
+            const unsigned long long nw = ((unsigned long long)tag << 32) | (unsigned long long)(cur + 1u);
+            const unsigned long long prev = atomicCAS(h, old, nw);
+            if (prev == old) { pos = cur; break; }
+            old = prev;
         }
-    }
-
-    S3R_GWT(2);
-    // exact row and segment starts
-    const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
-    const uint32_t y = row_of(lr);
-    if (lr >= rows_local || y < ymin || y > ymax || y >= H) { S3R_GWT_END(); return; }
-#if defined(S3R_GEO_ABLATE)                  // 2 = no walks at all
-    if (S3R_GEO_ABLATE & 2) return;
-#endif
-    const uint32_t nst = start_entries_of(W);
-    float *row = rowtab + ((size_t)slot * rows_local + lr) * nst * 4 + c;
-    const float d = sts.dx[c];
-#ifdef S3R_STATS
-    uint32_t it_row = 0, it_seg = 0;
-    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin, &it_row);
-#else
-    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
-#endif
-    row[0] = v;
-#if defined(S3R_GEO_ABLATE)                  // timing-only variants: 1 = no segment starts
-    if (S3R_GEO_ABLATE & 1) return;
-#endif
-    uint32_t xp = xmin;
-    for (uint32_t sg = xmin / kStartPx + 1u; sg + 1u < nst; sg++) {
-        const uint32_t xb = sg * kStartPx;
-        if (xb > xmax) break;
-#ifdef S3R_STATS
-        v = exact_walk(v, d, xb - xp, &it_seg);
-#else
-        v = exact_walk(v, d, xb - xp);
-#endif
-        xp = xb;
-        row[(1 + sg) * 4] = v;
+        if (pos >= kPairMax) continue;           // the fragment workgroup scans the slots itself
+        uint32_t k;
+        const uint32_t j = start_index(xmin, x0, &k);
+        float st[kWaves * 3];
+#pragma unroll
+        for (uint32_t r = 0; r < kWaves; r++) {
+            const uint32_t lr = lr0 + r, yy = row_of(lr);
+            const bool in = lr < rows_local && yy >= ymin && yy <= ymax && yy < H;
+            const float *rt = rowtab + (((size_t)slot * rows_local + lr) * nst + j) * 4;
+#pragma unroll
+            for (uint32_t c = 0; c < 3; c++) st[r * 3 + c] = in ? rt[c] : 0.0f;
+        }
+        uint4 *pr = pairs + (bin * kPairMax + pos) * kPairWords;
+        pr[0] = make_uint4(slot, xmin, xmax, ymin);
+        pr[1] = make_uint4(ymax, 0u, 0u, 0u);
+        pr[2] = make_uint4(f2u(sts.dx[0]), f2u(sts.dx[1]), f2u(sts.dx[2]), 0u);
+        pr[3] = make_uint4(f2u(sts.rvz[0]), f2u(sts.rvz[1]), f2u(sts.rvz[2]), 0u);
+#pragma unroll
+        for (uint32_t w = 0; w < 3; w++)
+            pr[4 + w] = make_uint4(f2u(st[4 * w]), f2u(st[4 * w + 1]), f2u(st[4 * w + 2]), f2u(st[4 * w + 3]));
     }
 #ifdef S3R_STATS
     const unsigned long long t_end = wall_clock64();
     atomicMax(&g_tstats[1], t_end - t_start);
     atomicMax(&g_tstats[3], t_end);
-    atomicAdd(&g_stats[12], (unsigned long long)it_row);
-    atomicMax(&g_stats[13], (unsigned long long)it_row);
-    atomicAdd(&g_stats[14], (unsigned long long)it_seg);
-    atomicMax(&g_stats[15], (unsigned long long)it_seg);
 #endif
     S3R_GWT_END();
 }
@@ -898,8 +930,8 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
                                                   uint32_t rows_local,
-                                                  const unsigned long long *__restrict__ binmask,
-                                                  uint32_t nwords, uint32_t done_tag, uint32_t *done_flag,
+                                                  const unsigned long long *__restrict__ binhdr,
+                                                  const uint4 *__restrict__ pairs, uint32_t done_tag, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order) {
     __shared__ FragShared sh;
     S3R_WGT(0);
@@ -936,35 +968,22 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     uint32_t *p_chunk = &st_chunk, *p_pix = &st_pix;
 #endif
 
-    // this workgroup's triangle list: the set bits of its slot mask (k_geometry), in slot order --
-    // or, beyond kListMax triangles, the first round of an in-kernel slot scan
-    bool overflow;
+    // this workgroup's triangle list: its bin's pairs (k_geometry), put in slot order -- or, beyond
+    // kPairMax triangles, the first round of an in-kernel slot scan.  Wave 0 fetches the first
+    // 64 / kPairWords pairs speculatively with the header (one round trip for most bins); the staging
+    // area is the exact-table space, unused until the chunk loop.
+    bool overflow = false;
+    uint4 *stage = reinterpret_cast<uint4 *>(&sh.tab4[0][0][0]);
+    const uint4 *pp = pairs + (size_t)bid * kPairMax * kPairWords;
     if (wave == 0) {
-        const unsigned long long *mw = binmask + (size_t)bid * nwords;
-        uint32_t cnt = 0;
-        for (uint32_t base = 0; base < nwords; base += 64u) {
-            const uint32_t i = base + lane;
-            const unsigned long long tw = i < nwords ? mw[i] : 0ull;
-            uint32_t w = (uint32_t)(tw >> 32) == done_tag ? (uint32_t)tw : 0u;   // this frame's bits only
-            const uint32_t pc = (uint32_t)__builtin_popcount(w);
-            uint32_t inc = pc;
-            for (uint32_t o = 1; o < 64u; o <<= 1) {
-                const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
-                if (lane >= o) inc += v;
-            }
-            uint32_t pos = cnt + inc - pc;
-            while (w) {
-                const uint32_t b = (uint32_t)__builtin_ctz(w);
-                w &= w - 1u;
-                if (pos < kListMax) sh.ent[pos].slot = i * 32u + b;
-                pos++;
-            }
-            cnt += rdl(inc, 63u);
-        }
-        if (lane == 0) sh.cnt = cnt;
+        stage[lane] = pp[lane];
+    } else if (wave == 1 && lane == 0) {
+        const unsigned long long hv = binhdr[bid];
+        sh.cnt = (uint32_t)(hv >> 32) == done_tag ? (uint32_t)hv : 0u;   // this frame's pairs only
     }
     __syncthreads();
-    if (sh.cnt == 0) {
+    const uint32_t npairs = sh.cnt;
+    if (npairs == 0) {
         // no triangle meets this block (sky): background only (render.cpp:282), 16 B per lane where
         // the row segment is 16-B aligned
         if (row_ok) {
@@ -982,47 +1001,44 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
         if (order && threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
         return;
     }
-    // batch 0's walk state, fetched speculatively with the raster constants: the start-table index
-    // is 0 (at xmin) or 1 + xs / kStartPx (start_index), so both candidates are read now and the
-    // entry's xmin picks one after load_entries (one dependent round trip less per workgroup)
-    float spec0 = 0.0f, spec1 = 0.0f;
-    if (sh.cnt <= kListMax && row_ok && lane < 63 && tl < sh.cnt) {
-        const size_t sb = ((size_t)sh.ent[tl].slot * rows_local + lr) * nst;
-        spec0 = rowtab[sb * 4 + comp];
-        spec1 = rowtab[(sb + 1u + xs / kStartPx) * 4 + comp];
-    }
-    if (sh.cnt <= kListMax) {
-        load_entries(tris, sh, sh.cnt, wave, lane);
-        overflow = false;
-    } else {
-        // > kListMax triangles meet this workgroup: stateless rounds of in-kernel slot scans
+    if (npairs > kPairMax) {
+        // > kPairMax triangles meet this workgroup: stateless rounds of in-kernel slot scans
         build_list(tris, nslots, y0, y1, xs, xe, 0, sh, wave, lane);
         overflow = true;
+    } else {
+        for (uint32_t i = 64u + threadIdx.x; i < npairs * kPairWords; i += 64u * kWaves) stage[i] = pp[i];
+        if (npairs * kPairWords > 64u) __syncthreads();
+        // pair i goes to list position rank(i) = the number of listed slots below its slot (the
+        // reference's processing order); its walk state to the batch lanes of that position
+        if (threadIdx.x < npairs) {
+            const uint4 *me = stage + threadIdx.x * kPairWords;
+            const uint4 h0 = me[0], h1 = me[1], dxw = me[2], rzw = me[3];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < npairs; j++) rank += stage[j * kPairWords].x < h0.x ? 1u : 0u;
+            Entry &e = sh.ent[rank];
+            e.slot = h0.x; e.xmin = h0.y; e.xmax = h0.z; e.ymin = h0.w; e.ymax = h1.x;
+            e.dx[0] = u2f(dxw.x); e.dx[1] = u2f(dxw.y); e.dx[2] = u2f(dxw.z);
+            e.rvz[0] = u2f(rzw.x); e.rvz[1] = u2f(rzw.y); e.rvz[2] = u2f(rzw.z);
+            const uint32_t b = rank / kTPB, lb = 3u * (rank - b * kTPB);
+            if (b < kStateBatches) {
+                uint32_t k;
+                (void)start_index(h0.y, xs, &k);
+                const uint4 s0 = me[4], s1 = me[5], s2 = me[6];
+                const float stv[kWaves * 3] = {u2f(s0.x), u2f(s0.y), u2f(s0.z), u2f(s0.w), u2f(s1.x), u2f(s1.y),
+                                               u2f(s1.z), u2f(s1.w), u2f(s2.x), u2f(s2.y), u2f(s2.z), u2f(s2.w)};
+#pragma unroll
+                for (uint32_t w = 0; w < kWaves; w++)
+#pragma unroll
+                    for (uint32_t c = 0; c < 3; c++) {
+                        sh.st_c[w][b * 64 + lb + c] = stv[w * 3 + c];
+                        sh.st_k[w][b * 64 + lb + c] = k;
+                    }
+            }
+        }
+        __syncthreads();
     }
     const uint32_t n0 = sh.cnt;
     S3R_WGT(1);
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 16)
-    if (false) {
-#else
-    if (!overflow && row_ok) {
-#endif
-        // walk state of the first batches: the exact value AT each listed triangle's first pixel in
-        // the segment, or at the last start-table point before it
-        for (uint32_t b = 0; b < kStateBatches && b * kTPB < n0; b++) {
-            const uint32_t idx = b * kTPB + tl;
-            if (lane < 63 && idx < n0) {
-                const Entry &e = sh.ent[idx];
-                if (y >= e.ymin && y <= e.ymax) {
-                    uint32_t k;
-                    const uint32_t j = start_index(e.xmin, xs, &k);
-                    st_c[b * 64 + lane] = b == 0 ? (j == 0 ? spec0 : spec1)
-                                                 : rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
-                    st_k[b * 64 + lane] = k;
-                }
-            }
-        }
-        wave_sync();
-    }
     S3R_WGT(2);
 
     // ---- batch 0 (the first kTPB listed triangles: nearly every row has no more) keeps its
@@ -1917,13 +1933,12 @@ uint32_t fragment_segments(uint32_t W) { return (W + kChunk * g_segch - 1) / (kC
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
     return (uint64_t)((rows_local + kWaves - 1) / kWaves) * fragment_segments(W);
 }
-uint32_t bin_words(uint32_t nslots) { return (nslots + 31u) / 32u; }
 
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done, uint32_t *order) {
+                     TriSetup *tris, float *rowtab, unsigned long long *binhdr, uint4 *pairs, uint32_t tag,
+                     hipStream_t st, hipEvent_t done, uint32_t *order) {
     if (ntri == 0 || rows_local == 0) {
         if (done) (void)hipEventRecord(done, st);
         return;
@@ -1931,15 +1946,14 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri + (order ? 1u : 0u), (rows_local + kGeoRows - 1) / kGeoRows),
                           dim3(3 * kGeoRows), 0, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor,
-                          W, H, band, nparts, part, rows_local, fragment_segments(W), kChunk * g_segch,
-                          bin_words(2 * ntri), tris, rowtab, binmask, tag, (uint32_t)fragment_bins(W, rows_local),
-                          order);
+                          W, H, band, nparts, part, rows_local, fragment_segments(W), kChunk * g_segch, tris, rowtab,
+                          binhdr, pairs, tag, (uint32_t)fragment_bins(W, rows_local), order);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, const unsigned long long *binmask, uint32_t tag, hipStream_t st,
-                     hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
+                     uint32_t rows_local, const unsigned long long *binhdr, const uint4 *pairs, uint32_t tag,
+                     hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -1949,12 +1963,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
-                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binmask,
-                              bin_words(nslots), tag, done_flag, prev_tag, order);
+                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binhdr, pairs, tag,
+                              done_flag, prev_tag, order);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
-                           W, H, band, nparts, part, segs, rows_local, binmask, bin_words(nslots), tag, done_flag,
-                           prev_tag, order);
+                           W, H, band, nparts, part, segs, rows_local, binhdr, pairs, tag, done_flag, prev_tag, order);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
