@@ -529,9 +529,10 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     const uint8_t *__restrict__ disc, const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx,
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
-    float *__restrict__ rowtab, unsigned long long *__restrict__ binhdr, uint4 *__restrict__ pairs, uint32_t tag,
+    float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
     uint32_t nbins, uint32_t *__restrict__ order) {
     __shared__ TriSetup sts;
+    extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
     const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
     if (slot >= 2u * ntri) {                   // the extra column: this frame's fragment order
         if (rb == 0) order_bins(order + nbins, nbins, order);
@@ -556,106 +557,108 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     if (sts.kind == kDead) { S3R_GWT_END(); return; }
     const uint32_t xmin = sts.xmin, xmax = sts.xmax, ymin = sts.ymin, ymax = sts.ymax;
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
-    const uint32_t nst = start_entries_of(W);
+
+    // bins of this workgroup's rows: (kGeoRows / kWaves) fragment row blocks x segs segments.  The
+    // slot takes the next pair of every bin its bbox meets (the count is reset by the bin's fragment
+    // workgroup, the last reader of this buffer set) and writes its raster constants there; the walks
+    // below add the exact walk state of the bin's rows.  Four bins per thread per step, so their
+    // atomics are in flight together.
+    const uint32_t nbr = kGeoRows / kWaves, nq = nbr * segs;
+    constexpr uint32_t kQ = 4;
+    for (uint32_t q0 = 0; q0 < nq; q0 += kQ * 3 * kGeoRows) {
+        uint32_t pos[kQ];
+#pragma unroll
+        for (uint32_t u = 0; u < kQ; u++) {
+            const uint32_t q = q0 + u * 3 * kGeoRows + tid;
+            pos[u] = kPairMax;
+            if (q >= nq) continue;
+            const uint32_t blk = rb * nbr + q / segs, sg = q % segs;
+            const uint32_t lr0 = blk * kWaves;
+            if (lr0 >= rows_local) continue;
+            uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
+            for (uint32_t k = 0; k < kWaves && lr0 + k < rows_local; k++) {
+                const uint32_t yy = row_of(lr0 + k);
+                y0 = min(y0, yy); y1 = max(y1, yy);
+            }
+            const uint32_t x0 = sg * segw, x1 = min(W, x0 + segw) - 1u;
+            if (ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)
+                pos[u] = atomicAdd(&bincnt[(size_t)blk * segs + sg], 1u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kQ; u++) {
+            const uint32_t q = q0 + u * 3 * kGeoRows + tid;
+            if (q >= nq) continue;
+            posmap[q] = pos[u] < kPairMax ? (uint8_t)pos[u] : (uint8_t)0xFF;
+            if (pos[u] < kPairMax) {
+                const size_t bin = (size_t)(rb * nbr + q / segs) * segs + q % segs;
+                uint4 *pr = pairs + (bin * kPairMax + pos[u]) * kPairWords;
+                pr[0] = make_uint4(slot, xmin, xmax, ymin);
+                pr[1] = make_uint4(ymax, 0u, 0u, 0u);
+                pr[2] = make_uint4(f2u(sts.dx[0]), f2u(sts.dx[1]), f2u(sts.dx[2]), 0u);
+                pr[3] = make_uint4(f2u(sts.rvz[0]), f2u(sts.rvz[1]), f2u(sts.rvz[2]), 0u);
+            }
+        }
+    }
+    __syncthreads();
+    S3R_GWT(2);
 
     // exact row and start-table points: lane (row, component) walks the reference's sequence exactly
     // (exact_walk): wy += dy down to its row (render.cpp:378), then w += dx along the row through every
-    // kStartPx boundary inside the bbox (:374)
-    {
-        const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
-        const uint32_t y = row_of(lr);
-        bool walk_row = !(lr >= rows_local || y < ymin || y > ymax || y >= H);
+    // kStartPx boundary inside the bbox (:374); each value goes to the start table and to the pairs of
+    // the fragment segments whose walks start there (start_index)
+    const uint32_t c = tid / kGeoRows, lr = rb * kGeoRows + tid % kGeoRows;
+    const uint32_t y = row_of(lr);
+    if (lr >= rows_local || y < ymin || y > ymax || y >= H) { S3R_GWT_END(); return; }
 #if defined(S3R_GEO_ABLATE)                  // 2 = no walks at all
-        if (S3R_GEO_ABLATE & 2) walk_row = false;
+    if (S3R_GEO_ABLATE & 2) return;
 #endif
-        if (walk_row) {
-            float *row = rowtab + ((size_t)slot * rows_local + lr) * nst * 4 + c;
-            const float d = sts.dx[c];
+    const uint32_t nst = start_entries_of(W);
+    float *row = rowtab + ((size_t)slot * rows_local + lr) * nst * 4 + c;
+    const uint8_t *pm = posmap + (lr / kWaves - rb * nbr) * segs;
+    float *pst = reinterpret_cast<float *>(pairs) + 16u + (lr % kWaves) * 3u + c;   // state float in pair 0
+    const size_t bin0 = (size_t)(lr / kWaves) * segs;
+    // the fragment segments [sg, sg_end) take their walk state from value v
+    auto to_pairs = [&](uint32_t sg, uint32_t sg_end, float v) {
+        for (; sg < sg_end && sg < segs; sg++) {
+            const uint32_t pq = pm[sg];
+            if (pq != 0xFFu) pst[((bin0 + sg) * kPairMax + pq) * (kPairWords * 4u)] = v;
+        }
+    };
+    const float d = sts.dx[c];
 #ifdef S3R_STATS
-            uint32_t it_row = 0, it_seg = 0;
-            float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin, &it_row);
+    uint32_t it_row = 0, it_seg = 0;
+    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin, &it_row);
 #else
-            float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
+    float v = exact_walk(sts.ws[c], sts.dy[c], y - ymin);
 #endif
-            row[0] = v;
-            uint32_t xp = xmin;
+    row[0] = v;
+    // segments starting at or before the first start-table boundary past xmin walk from the row start
+    const uint32_t sg_xmin = xmin / segw, b1 = (xmin / kStartPx + 1u) * kStartPx;
+    to_pairs(sg_xmin, min((xmax / segw) + 1u, b1 / segw), v);
 #if defined(S3R_GEO_ABLATE)                  // timing-only variants: 1 = no segment starts
-            if (!(S3R_GEO_ABLATE & 1))
+    if (S3R_GEO_ABLATE & 1) return;
 #endif
-            for (uint32_t sg = xmin / kStartPx + 1u; sg + 1u < nst; sg++) {
-                const uint32_t xb = sg * kStartPx;
-                if (xb > xmax) break;
+    uint32_t xp = xmin;
+    for (uint32_t sb = xmin / kStartPx + 1u; sb + 1u < nst; sb++) {
+        const uint32_t xb = sb * kStartPx;
+        if (xb > xmax) break;
 #ifdef S3R_STATS
-                v = exact_walk(v, d, xb - xp, &it_seg);
+        v = exact_walk(v, d, xb - xp, &it_seg);
 #else
-                v = exact_walk(v, d, xb - xp);
+        v = exact_walk(v, d, xb - xp);
 #endif
-                xp = xb;
-                row[(1 + sg) * 4] = v;
-            }
-#ifdef S3R_STATS
-            atomicAdd(&g_stats[12], (unsigned long long)it_row);
-            atomicMax(&g_stats[13], (unsigned long long)it_row);
-            atomicAdd(&g_stats[14], (unsigned long long)it_seg);
-            atomicMax(&g_stats[15], (unsigned long long)it_seg);
-#endif
-        }
-    }
-    __syncthreads();                           // this workgroup's rowtab rows are written
-    S3R_GWT(2);
-
-    // bins of this workgroup's rows: (kGeoRows / kWaves) fragment row blocks x segs segments.  The
-    // slot takes the next pair of every bin its bbox meets (tagged header: a header still carrying an
-    // older frame's tag counts as empty) and writes its raster constants and the exact walk state of
-    // the bin's rows there (the start-table point of the bin's first pixel, start_index)
-    const uint32_t nbr = kGeoRows / kWaves;
-    for (uint32_t q = tid; q < nbr * segs; q += 3 * kGeoRows) {
-        const uint32_t blk = rb * nbr + q / segs, sg = q % segs;
-        const uint32_t lr0 = blk * kWaves;
-        if (lr0 >= rows_local) continue;
-        uint32_t y0 = 0xFFFFFFFFu, y1 = 0;
-        for (uint32_t k = 0; k < kWaves && lr0 + k < rows_local; k++) {
-            const uint32_t yy = row_of(lr0 + k);
-            y0 = min(y0, yy); y1 = max(y1, yy);
-        }
-        const uint32_t x0 = sg * segw, x1 = min(W, x0 + segw) - 1u;
-        if (!(ymin <= y1 && ymax >= y0 && xmin <= x1 && xmax >= x0)) continue;
-        const size_t bin = (size_t)blk * segs + sg;
-        unsigned long long *h = &binhdr[bin];
-        unsigned long long old = *h;
-        uint32_t pos;
-        for (;;) {
-            const uint32_t cur = (uint32_t)(old >> 32) == tag ? (uint32_t)old : 0u;
-            const unsigned long long nw = ((unsigned long long)tag << 32) | (unsigned long long)(cur + 1u);
-            const unsigned long long prev = atomicCAS(h, old, nw);
-            if (prev == old) { pos = cur; break; }
-            old = prev;
-        }
-        if (pos >= kPairMax) continue;           // the fragment workgroup scans the slots itself
-        uint32_t k;
-        const uint32_t j = start_index(xmin, x0, &k);
-        float st[kWaves * 3];
-#pragma unroll
-        for (uint32_t r = 0; r < kWaves; r++) {
-            const uint32_t lr = lr0 + r, yy = row_of(lr);
-            const bool in = lr < rows_local && yy >= ymin && yy <= ymax && yy < H;
-            const float *rt = rowtab + (((size_t)slot * rows_local + lr) * nst + j) * 4;
-#pragma unroll
-            for (uint32_t c = 0; c < 3; c++) st[r * 3 + c] = in ? rt[c] : 0.0f;
-        }
-        uint4 *pr = pairs + (bin * kPairMax + pos) * kPairWords;
-        pr[0] = make_uint4(slot, xmin, xmax, ymin);
-        pr[1] = make_uint4(ymax, 0u, 0u, 0u);
-        pr[2] = make_uint4(f2u(sts.dx[0]), f2u(sts.dx[1]), f2u(sts.dx[2]), 0u);
-        pr[3] = make_uint4(f2u(sts.rvz[0]), f2u(sts.rvz[1]), f2u(sts.rvz[2]), 0u);
-#pragma unroll
-        for (uint32_t w = 0; w < 3; w++)
-            pr[4 + w] = make_uint4(f2u(st[4 * w]), f2u(st[4 * w + 1]), f2u(st[4 * w + 2]), f2u(st[4 * w + 3]));
+        xp = xb;
+        row[(1 + sb) * 4] = v;
+        to_pairs(xb / segw, min((xmax / segw) + 1u, (xb + kStartPx) / segw), v);
     }
 #ifdef S3R_STATS
     const unsigned long long t_end = wall_clock64();
     atomicMax(&g_tstats[1], t_end - t_start);
     atomicMax(&g_tstats[3], t_end);
+    atomicAdd(&g_stats[12], (unsigned long long)it_row);
+    atomicMax(&g_stats[13], (unsigned long long)it_row);
+    atomicAdd(&g_stats[14], (unsigned long long)it_seg);
+    atomicMax(&g_stats[15], (unsigned long long)it_seg);
 #endif
     S3R_GWT_END();
 }
@@ -930,7 +933,7 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
                                                   uint32_t rows_local,
-                                                  const unsigned long long *__restrict__ binhdr,
+                                                  uint32_t *__restrict__ bincnt,
                                                   const uint4 *__restrict__ pairs, uint32_t done_tag, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order) {
     __shared__ FragShared sh;
@@ -978,8 +981,10 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
     if (wave == 0) {
         stage[lane] = pp[lane];
     } else if (wave == 1 && lane == 0) {
-        const unsigned long long hv = binhdr[bid];
-        sh.cnt = (uint32_t)(hv >> 32) == done_tag ? (uint32_t)hv : 0u;   // this frame's pairs only
+        // this frame's pair count; reset for the buffer set's next geometry (this launch is the set's
+        // last reader: the host issues that geometry only once this launch has completed)
+        sh.cnt = bincnt[bid];
+        bincnt[bid] = 0u;
     }
     __syncthreads();
     const uint32_t npairs = sh.cnt;
@@ -1937,22 +1942,24 @@ uint64_t fragment_bins(uint32_t W, uint32_t rows_local) {
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, unsigned long long *binhdr, uint4 *pairs, uint32_t tag,
-                     hipStream_t st, hipEvent_t done, uint32_t *order) {
+                     TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
+                     uint32_t *order) {
     if (ntri == 0 || rows_local == 0) {
         if (done) (void)hipEventRecord(done, st);
         return;
     }
     // the completion event is recorded by the launch itself (one host call instead of two)
+    // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
+    const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
     hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri + (order ? 1u : 0u), (rows_local + kGeoRows - 1) / kGeoRows),
-                          dim3(3 * kGeoRows), 0, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor,
-                          W, H, band, nparts, part, rows_local, fragment_segments(W), kChunk * g_segch, tris, rowtab,
-                          binhdr, pairs, tag, (uint32_t)fragment_bins(W, rows_local), order);
+                          dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
+                          m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, const unsigned long long *binhdr, const uint4 *pairs, uint32_t tag,
+                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs, uint32_t tag,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
@@ -1963,11 +1970,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
-                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, binhdr, pairs, tag,
+                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs, tag,
                               done_flag, prev_tag, order);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
-                           W, H, band, nparts, part, segs, rows_local, binhdr, pairs, tag, done_flag, prev_tag, order);
+                           W, H, band, nparts, part, segs, rows_local, bincnt, pairs, tag, done_flag, prev_tag, order);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

@@ -71,7 +71,7 @@ struct Lib {
     TriSetup *tris[kSets] = {};
     float *rowtab[kSets] = {};     // 2T x rows x (segments + 1) x float4 exact row starts
     size_t rowtab_cap = 0;
-    unsigned long long *binhdr[kSets] = {};  // per fragment workgroup (bin): tagged pair count
+    uint32_t *bincnt[kSets] = {};            // per fragment workgroup (bin): pair count (s3r_kernels.h)
     uint4 *pairs[kSets] = {};                // per bin: kPairMax pair records (s3r_kernels.h)
     uint64_t bins_cap = 0;
     // longest-first fragment order, per buffer set: [perm | cost] (s3r_kernels.h launch_fragment)
@@ -327,7 +327,7 @@ void release_all() {
         for (void *p : ptrs)
             if (p) (void)hipFree(p);
         for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
-            void *set[] = {g.tris[q], g.rowtab[q], g.binhdr[q], g.pairs[q], g.order[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
+            void *set[] = {g.tris[q], g.rowtab[q], g.bincnt[q], g.pairs[q], g.order[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
                            g.tile_list[q], g.recs[q], g.boxes[q], g.app_list[q], g.app_count[q]};
             for (void *p : set)
                 if (p) (void)hipFree(p);
@@ -392,7 +392,7 @@ constexpr uint32_t kTagLimit = 0xFFFFFF00u;
 void restart_tags(uint32_t next_frame_no) {
     HIPCHECK(hipDeviceSynchronize());
     for (int p = 0; p < kSets; p++)
-        if (g.binhdr[p]) HIPCHECK(hipMemset(g.binhdr[p], 0, g.bins_cap * sizeof(unsigned long long)));
+        if (g.bincnt[p]) HIPCHECK(hipMemset(g.bincnt[p], 0, g.bins_cap * sizeof(uint32_t)));
     HIPCHECK(hipDeviceSynchronize());
     g.frame_no = next_frame_no;
     for (uint32_t &t : g.issued_tag) t = 0;
@@ -555,14 +555,14 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     if (g.bins_cap < nbins) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
-            if (g.binhdr[p]) HIPCHECK(hipFree(g.binhdr[p]));
+            if (g.bincnt[p]) HIPCHECK(hipFree(g.bincnt[p]));
             if (g.pairs[p]) HIPCHECK(hipFree(g.pairs[p]));
-            g.binhdr[p] = dalloc<unsigned long long>(nbins);
+            g.bincnt[p] = dalloc<uint32_t>(nbins);
             g.pairs[p] = dalloc<uint4>(nbins * kPairMax * kPairWords);
-            HIPCHECK(hipMemset(g.binhdr[p], 0, nbins * sizeof(unsigned long long)));   // tag 0: no frame
+            HIPCHECK(hipMemset(g.bincnt[p], 0, nbins * sizeof(uint32_t)));
         }
         // hipMemset runs on the null stream, which does not order the non-blocking geometry
-        // streams: finish it before the next k_geometry counts pairs in these headers
+        // streams: finish it before the next k_geometry counts pairs in these bins
         HIPCHECK(hipDeviceSynchronize());
         g.bins_cap = nbins;
     }
@@ -596,7 +596,7 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     hp.lap(2);
     const uint32_t tag = g.frame_no;              // >= 1: frame k's tag for its slot masks and completion
     launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, g.tris[p], g.rowtab[p], g.binhdr[p], g.pairs[p], tag, geo, g.geo_done[p],
+                    rows_local, g.tris[p], g.rowtab[p], g.bincnt[p], g.pairs[p], geo, g.geo_done[p],
                     lpt ? g.order[p] : nullptr);
     hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
@@ -607,7 +607,7 @@ void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_
     hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.binhdr[p], g.pairs[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag,
+                    g.bincnt[p], g.pairs[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag,
                     lpt ? g.order[p] : nullptr);
     g.issued_tag[p] = tag;
     g.last_tag = tag;

@@ -14,16 +14,17 @@ namespace s3r {
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, const unsigned long long *binhdr, const uint4 *pairs, uint32_t tag,
+                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs, uint32_t tag,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
-// tagged header, (frame tag << 32) | count -- a header whose tag is not the frame's reads as an empty
-// bin, so nothing clears them (k_fragment only reads the buffer set, which is reusable as soon as its
-// last fragment kernel has counted out) -- and kPairMax pair records of kPairWords uint4 (128 B) in
-// arrival order: {slot, xmin, xmax, ymin}, {ymax, 0, 0, 0}, {dx[3], 0}, {1/z[3], 0}, then the exact
-// walk state of the bin's 4 rows x 3 components at the start-table point of the bin's first pixel
-// (row-major, 12 floats).  A bin met by more than kPairMax triangles scans the slots itself.
+// pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0
+// (the fragment launch is the buffer set's last reader, and the set's next geometry is issued only
+// once it has completed) -- and kPairMax pair records of kPairWords uint4 (128 B) in arrival order:
+// {slot, xmin, xmax, ymin}, {ymax, 0, 0, 0}, {dx[3], 0}, {1/z[3], 0}, then the exact walk state of the
+// bin's 4 rows x 3 components at the start-table point of the bin's first pixel (row-major, 12 floats;
+// rows outside the triangle's bbox are left unwritten).  A bin met by more than kPairMax triangles
+// scans the slots itself.
 constexpr uint32_t kPairMax = 64;
 constexpr uint32_t kPairWords = 8;
 uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
@@ -35,8 +36,8 @@ uint32_t start_entries(uint32_t W);
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                     TriSetup *tris, float *rowtab, unsigned long long *binhdr, uint4 *pairs, uint32_t tag,
-                     hipStream_t st, hipEvent_t done, uint32_t *order);
+                     TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
+                     uint32_t *order);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
