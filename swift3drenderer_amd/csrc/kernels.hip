@@ -273,18 +273,23 @@ __device__ unsigned long long g_gwt[kGeoTimesMax * 4];
 #endif
 
 // ------------------------------------------------------------------ ripmap sample
-__device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t base,
-                                          float u, float v, float lvx, float lvy) {
-    // getTextureColor, render.cpp:124-132
-    // levels clamped to [1, 256] (fminf(NaN, 256) = 256): the truncation needs no range guard and
-    // nextPowerOfTwo of i in [1, 256] is 1 << (32 - clz(i - 1)) for i > 1
+// getTextureColor's texel offset inside one 512 x 512 ripmap (render.cpp:124-132)
+__device__ __forceinline__ uint32_t texel_offset(float u, float v, float lvx, float lvy) {
     const uint32_t ix = (uint32_t)(int32_t)fmaxf(fminf(lvx, 256.f), 1.f);
     const uint32_t iy = (uint32_t)(int32_t)fmaxf(fminf(lvy, 256.f), 1.f);
     const uint32_t lx = ix > 1u ? 1u << (32u - (uint32_t)__builtin_clz(ix - 1u)) : 1u;
     const uint32_t ly = iy > 1u ? 1u << (32u - (uint32_t)__builtin_clz(iy - 1u)) : 1u;
     const uint32_t x = u32_of_float(frac1(u) * (float)lx) + (511u & ~(2u * lx - 1u));
     const uint32_t y = u32_of_float(frac1(v) * (float)ly) + (511u & ~(2u * ly - 1u));
-    const uint32_t off = (x + (y << 9)) & (kTexTexels - 1u);
+    return (x + (y << 9)) & (kTexTexels - 1u);
+}
+
+__device__ __forceinline__ uint32_t texel(const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t base,
+                                          float u, float v, float lvx, float lvy) {
+    // getTextureColor, render.cpp:124-132
+    // levels clamped to [1, 256] (fminf(NaN, 256) = 256): the truncation needs no range guard and
+    // nextPowerOfTwo of i in [1, 256] is 1 << (32 - clz(i - 1)) for i > 1
+    const uint32_t off = texel_offset(u, v, lvx, lvy);
     // Out-of-range texture index is UB in the reference; defined here (and in the oracle) as 0.
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 256)
     return off * 0x010101u + base;                 // ablation: no texel load
@@ -717,15 +722,13 @@ S3R_CALLEE uint32_t shade_core(float4 c0, float4 c1, float4 c2, float4 n0, float
 #ifndef S3R_SHADE_FLAT
 #define S3R_SHADE_FLAT 1
 #endif
-#ifndef S3R_TEX_EARLY
-#define S3R_TEX_EARLY 1
-#endif
 // shade_core as one straight-line block: every correctly rounded division and sqrt takes its trimmed
 // sequence unconditionally while the range conditions are collected in `ok`; a lane with any operand
 // out of range is shaded again by shade_core (same bits either way).  Without the per-operation
-// branches the scheduler interleaves the independent chains (the normalisations of P and N, the
-// texture coordinates and the texel load; a colour triangle's lanes compute the texture path too and
-// discard it, its texel index is masked in range).
+// branches the scheduler interleaves the independent chains.  The texel is loaded unconditionally as
+// soon as its coordinates exist (an index clamped to 0 where the reference's lookup would be out of
+// range or the triangle is coloured: the value is then discarded) and consumed only after the
+// normalisations, so its latency runs under them.
 S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0,
                                     float4 k1, float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1,
                                     float w2, float ooz, const uint32_t *__restrict__ tex, uint32_t ntex) {
@@ -743,9 +746,9 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     ok &= !texd | (inr(dvx) & inr(dvy));
     const float lvx = div_with_recip(ooz, dvx, div_recip(dvx));
     const float lvy = div_with_recip(ooz, dvy, div_recip(dvy));
-#if S3R_TEX_EARLY
-    const uint32_t rgb = texel(tex, ntex, tex_base, mu, mv, lvx, lvy);
-#endif
+    // out-of-range texture index: UB in the reference, 0 here and in the oracle (texel())
+    const bool tex_ok = texd & (tex_base < ntex) & (ntex - tex_base >= kTexTexels);
+    uint32_t rgb = tex[tex_ok ? tex_base + texel_offset(mu, mv, lvx, lvy) : 0u];
     auto norm = [&ok](F3 v) {
         const float d = dot3(v, v);
         ok &= sqrt_in_range_ok(d);
@@ -761,10 +764,11 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     const F3 normal = norm(N);
     const F3 point = mk3(-pn.x, -pn.y, -pn.z);
     const F3 halfway = norm(add3(point, normal));
-    const float s = dot3(halfway, normal);
-#if !S3R_TEX_EARLY
-    const uint32_t rgb = texel(tex, ntex, tex_base, mu, mv, lvx, lvy);
-#endif
+    float s = dot3(halfway, normal);
+    // the texel is consumed from here on: keeps the compiler from waiting for it before the
+    // normalisations above
+    asm volatile("" : "+v"(rgb), "+v"(s));
+    rgb = tex_ok ? rgb : 0u;
     const F3 col = texd ? mk3((float)(rgb >> 16), (float)((rgb >> 8) & 255u), (float)(rgb & 255u))
                         : mk3((k0.x * a + k1.x * b) + k2.x * c, (k0.y * a + k1.y * b) + k2.y * c,
                               (k0.z * a + k1.z * b) + k2.z * c);
