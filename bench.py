@@ -191,11 +191,27 @@ def main():
 
     # the same frames reassembled on rank 0 by one gather per frame (reported beside value)
     gathered_fps = None
+    e2e_multi = None
     if N > 1:
         for _ in range(3):
             gathered(hold)
         kg = max(10, min(100, a.steps))
         gathered_fps = kg / timed(gathered, kg)
+        # the same frames delivered into ONE host frame shared by the node's ranks (/dev/shm), each
+        # rank copying its own bands over its own GPU's PCIe link (s3r_bands_to_host): the
+        # multi-GPU counterpart of updateAndRender's host buffer
+        from swift3drenderer_amd.multi import HostFrame
+        hf = HostFrame(W, H, rank)
+        src = bg.send if a.backend == 'nccl' else local_buf
+
+        def delivered(inp):
+            render(inp)
+            r.bands_to_host(src.data_ptr(), W, H, B, N, rank, hf.frame, sptr)
+
+        for _ in range(3):
+            delivered(hold)
+        e2e_multi = kg / timed(delivered, kg)
+        hf.close()
 
     fps = a.steps / el
     counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
@@ -257,7 +273,8 @@ def main():
             'mpixels_per_s': round(fps * W * H / 1e6, 2),
             'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
             'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
-            'e2e_fps_with_d2h': round(e2e, 3) if e2e else None,
+            # N = 1: updateAndRender into a host buffer; N > 1: every rank's bands into one shared host frame
+            'e2e_fps_with_d2h': round(e2e, 3) if e2e else (round(e2e_multi, 3) if e2e_multi else None),
             'gathered_fps': round(gathered_fps, 3) if gathered_fps else None,
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),

@@ -1441,10 +1441,12 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
                 if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) {
                     TriSetup ta;
                     if (raster_part(app, sw, sh, ta)) {
-                        write_rec(recs + ntri + t, ta, ntri + t);
-                        app_list[atomicAdd(app_count, 1u)] = ntri + t;
                         const TileSpan sa = box_tiles(ta.xmin | (ta.xmax << 16), ta.ymin | (ta.ymax << 16), band,
                                                       nparts, part);
+                        if (sa.n) {                     // only triangles meeting this part's rows
+                            write_rec(recs + ntri + t, ta, ntri + t);
+                            app_list[atomicAdd(app_count, 1u)] = ntri + t;
+                        }
                         for (uint32_t k = 0; k < sa.n; k++)
                             atomicAdd(&counts[(sa.ty0 + k / sa.ntx) * tiles_x + sa.tx0 + k % sa.ntx], 1u);
                     }
@@ -1454,16 +1456,21 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
         }
     }
     uint32_t bx = kDeadBox, by = 0;
+    TileSpan sp{0, 1, 0, 0};
     if (live) {
-        bx = ts.xmin | (ts.xmax << 16);
-        by = ts.ymin | (ts.ymax << 16);
-        write_rec(recs + t, ts, t);
+        sp = box_tiles(ts.xmin | (ts.xmax << 16), ts.ymin | (ts.ymax << 16), band, nparts, part);
+        // a triangle outside this part's rows (row-band split) is dead here: no record, no box
+        if (sp.n) {
+            bx = ts.xmin | (ts.xmax << 16);
+            by = ts.ymin | (ts.ymax << 16);
+            write_rec(recs + t, ts, t);
+        }
     }
     if (in) reinterpret_cast<uint2 *>(boxes)[t] = make_uint2(bx, by);
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 1)
     if (bx == 12345u)                                   // ablation: no tile counting
 #endif
-    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, counts, nullptr, 0);
+    tile_visit(sp, tiles_x, counts, nullptr, 0);
 }
 
 // Exclusive scan of the tile counts (one workgroup): offs[t], cursor[t] = offs[t], *total.

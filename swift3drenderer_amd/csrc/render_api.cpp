@@ -748,6 +748,30 @@ __attribute__((visibility("default"))) void s3r_debug_set_frame_count(uint32_t f
     restart_tags(frame_no > kTagLimit ? kTagLimit : frame_no);
 }
 
+__attribute__((visibility("default"))) int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t height,
+                                                                uint32_t band_rows, uint32_t n_parts, uint32_t part,
+                                                                uint32_t *host_frame, void *stream) {
+    if (band_rows == 0 || n_parts == 0 || part >= n_parts || ((!dev_rows || !host_frame) && width && height)) return -1;
+    const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
+    if (!rows || !width) return rows;
+    if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
+    host_pinned(host_frame, (size_t)width * height * sizeof(uint32_t));
+    hipStream_t st = (hipStream_t)stream;
+    const size_t rowb = (size_t)width * sizeof(uint32_t);
+    // this part's bands: b = part, part + n_parts, ...; all full except perhaps the frame's last band
+    const uint32_t nbands = (height + band_rows - 1) / band_rows, last = nbands - 1u;
+    const uint32_t mine = (nbands > part) ? (nbands - part + n_parts - 1u) / n_parts : 0u;
+    const bool partial_last = (uint64_t)nbands * band_rows > height && last % n_parts == part;
+    const uint32_t full = mine - (partial_last ? 1u : 0u);
+    if (full)
+        HIPCHECK(hipMemcpy2DAsync(host_frame + (size_t)part * band_rows * width, (size_t)n_parts * band_rows * rowb, dev_rows,
+                                  (size_t)band_rows * rowb, (size_t)band_rows * rowb, full, hipMemcpyDeviceToHost, st));
+    if (partial_last)
+        HIPCHECK(hipMemcpyAsync(host_frame + (size_t)last * band_rows * width, dev_rows + (size_t)full * band_rows * width,
+                                (size_t)(height - last * band_rows) * rowb, hipMemcpyDeviceToHost, st));
+    return rows;
+}
+
 __attribute__((visibility("default"))) void s3r_timing(int enable) {
     g.timing = enable != 0;
     g.tcount = 0;

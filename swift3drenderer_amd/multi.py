@@ -53,6 +53,39 @@ class BandGather:
         return self.frame
 
 
+class HostFrame:
+    """One H x W uint32 host frame shared by all ranks of a node (a file in /dev/shm, mapped by every
+    process): the destination of s3r_bands_to_host, each rank copying its own bands over its own
+    GPU's PCIe link (the direct-D2H alternative to the gather).  Collective: every
+    rank constructs and closes it."""
+
+    def __init__(self, width: int, height: int, rank: int, group=None):
+        import os
+        import uuid
+        self.rank = rank
+        name = [f'/dev/shm/s3r_frame_{os.getpid()}_{uuid.uuid4().hex[:12]}' if rank == 0 else None]
+        if dist.is_available() and dist.is_initialized():
+            dist.broadcast_object_list(name, src=0, group=group)
+        self.path = name[0]
+        if rank == 0:
+            with open(self.path, 'wb') as f:
+                f.truncate(width * height * 4)
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier(group=group)
+        self.frame = np.memmap(self.path, dtype=np.uint32, mode='r+', shape=(height, width))
+
+    def close(self, group=None):
+        self.frame._mmap.close()
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier(group=group)
+        if self.rank == 0:
+            import os
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
 def assemble(parts, height: int, band: int) -> np.ndarray:
     """Host-side reassembly of per-part compact buffers (tests and single-process use)."""
     n = len(parts)

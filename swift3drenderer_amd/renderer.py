@@ -51,6 +51,9 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double)]
     lib.s3r_scene_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_camera.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.s3r_bands_to_host.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    lib.s3r_bands_to_host.restype = ctypes.c_int64
     lib.s3r_debug_set_frame_count.argtypes = [ctypes.c_uint32]
     lib.s3r_debug_set_frame_count.restype = None
     _lib = lib
@@ -103,6 +106,18 @@ class Renderer:
                                       ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None))
         if r < 0:
             raise ValueError('s3r_render_bands: bad arguments')
+        return int(r)
+
+    def bands_to_host(self, dev_ptr: int, width: int, height: int, band: int, nparts: int, part: int,
+                      host: np.ndarray, stream: int = 0) -> int:
+        """Copy one part's rows (device, compact) into their rows of the host frame `host` (H x W
+        uint32, C-contiguous) on `stream`, asynchronously (s3r_bands_to_host)."""
+        if host.dtype != np.uint32 or host.shape != (height, width) or not host.flags['C_CONTIGUOUS']:
+            raise ValueError('host frame must be a C-contiguous (height, width) uint32 array')
+        r = self.lib.s3r_bands_to_host(ctypes.c_void_p(dev_ptr), width, height, band, nparts, part,
+                                       ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(stream or None))
+        if r < 0:
+            raise ValueError('s3r_bands_to_host: bad arguments')
         return int(r)
 
     def set_raster_path(self, mode: str | int):

@@ -110,3 +110,84 @@ def test_gpu_band_parts_reassemble(gpu_renderer, scene_dir, nparts, band):
         bad_parts = sorted({(int(y) // band) % nparts for y in ys})
         raise AssertionError(f'{len(ys)} pixels differ (rows {ys.min()}-{ys.max()}, parts {bad_parts}); first at '
                              f'(x={xs[0]}, y={ys[0]}): parts {got[ys[0], xs[0]]:#x} whole frame {want[ys[0], xs[0]]:#x}')
+
+
+def _host_frame_worker(rank, world, port, frame, band, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from swift3drenderer_amd.multi import HostFrame
+    h, w = frame.shape
+    hf = HostFrame(w, h, rank)
+    ids = band_row_ids(h, band, world, rank)
+    hf.frame[ids] = frame[ids]                 # what s3r_bands_to_host delivers for this rank
+    dist.barrier()
+    if rank == 0:
+        q.put(np.array(hf.frame))
+    hf.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,band', [(2, 16), (3, 5)])
+def test_gloo_shared_host_frame(world, band):
+    """Every rank writes its bands into the node-shared host frame (/dev/shm): rank 0 sees the whole
+    frame, and the file is gone afterwards."""
+    import glob
+    rng = np.random.default_rng(world)
+    frame = rng.integers(0, 2 ** 24, (70, 33), dtype=np.uint32)
+    before = set(glob.glob('/dev/shm/s3r_frame_*'))
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_host_frame_worker, args=(r, world, port, frame, band, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got, frame)
+    assert set(glob.glob('/dev/shm/s3r_frame_*')) == before
+
+
+def test_bands_to_host_rejects_bad_arguments():
+    import ctypes
+    from swift3drenderer_amd.renderer import load_library
+    lib = load_library()
+    buf = np.zeros((4, 4), dtype=np.uint32)
+    assert lib.s3r_bands_to_host(None, 4, 4, 0, 1, 0, buf.ctypes.data_as(ctypes.c_void_p), None) == -1
+    assert lib.s3r_bands_to_host(None, 4, 4, 2, 2, 2, buf.ctypes.data_as(ctypes.c_void_p), None) == -1
+    assert lib.s3r_bands_to_host(None, 4, 4, 2, 2, 0, None, None) == -1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W,H,nparts,band', [(800, 600, 3, 16), (3840, 2160, 8, 16), (641, 97, 4, 7), (320, 240, 1, 240)])
+def test_gpu_bands_to_host_frame(gpu_renderer, scene_dir, W, H, nparts, band):
+    """Each part rendered on the GPU and delivered straight into its rows of one host frame
+    (s3r_bands_to_host): the assembled host frame equals the oracle's, bit for bit, and rows of the
+    frame no part owns are never written."""
+    from oracle.oracle import render_pose as oracle_render_pose
+    from swift3drenderer_amd import poses
+    r = gpu_renderer
+    dev = torch.device('cuda', 0)
+    script = poses.script('P_over')
+    want = oracle_render_pose(scene_dir['full'], script, W, H)
+    r.configure(scene_dir['full'])
+    st = torch.cuda.current_stream(dev).cuda_stream
+    scratch = torch.empty((H, W), dtype=torch.int32, device=dev)
+    for t in script:
+        r.render_bands(t, W, H, H, 1, 0, scratch.data_ptr(), st)
+    host = np.full((H, W), 0xDEADBEEF, dtype=np.uint32)
+    hold = poses.hold('P_over')
+    bufs = []
+    for p in range(nparts):
+        rows = band_rows(H, band, nparts, p)
+        buf = torch.full((max(rows, 1), W), -1, dtype=torch.int32, device=dev)
+        r.render_bands(hold, W, H, band, nparts, p, buf.data_ptr(), st)
+        assert r.bands_to_host(buf.data_ptr(), W, H, band, nparts, p, host, st) == rows
+        bufs.append(buf)
+    torch.cuda.synchronize()
+    if not np.array_equal(host, want):
+        ys, xs = np.nonzero(host != want)
+        raise AssertionError(f'{len(ys)} pixels differ; first at (x={xs[0]}, y={ys[0]}): host {host[ys[0], xs[0]]:#x} '
+                             f'oracle {want[ys[0], xs[0]]:#x}')
