@@ -25,14 +25,15 @@ def main():
     p.add_argument('--steps', type=int, default=400)
     p.add_argument('--nparts', type=int, default=1, help='emulate one rank of an N-GPU band split')
     p.add_argument('--band', type=int, default=16)
+    p.add_argument('--data', default=None, help='use (and create if missing) this data.bin instead of a temp file')
     a = p.parse_args()
     import torch
     from swift3drenderer_amd import poses, scene
     from swift3drenderer_amd.renderer import Renderer
     torch.cuda.set_device(0)
-    d = tempfile.mkdtemp()
-    path = os.path.join(d, 's.bin')
-    scene.write_named(a.scene, path)
+    path = a.data or os.path.join(tempfile.mkdtemp(), 's.bin')
+    if not os.path.exists(path):
+        scene.write_named(a.scene, path)
     W, H = a.width, a.height
     r = Renderer(path, device=0)
     N, B = a.nparts, (a.band if a.nparts > 1 else H)
