@@ -1929,14 +1929,19 @@ static_assert(kSegChunks == 6, "k_fragment instantiations below: 6, 3, 2, 1 chun
 // Segment width of this frame's row path: the widest of 6, 3, 2, 1 chunks that still launches at
 // least kMinFragBlocks workgroups (~8 per CU), so small frames fill the chip (a 1080p frame at
 // 6 chunks is 1350 workgroups; each runs a latency-bound chain, so too few leave CUs idle).
+// Widths tried: 6, 2, 1 chunks.  Round-2 sweep (tools/knob_sweep.sh, tools/part_knobs.sh): where
+// 3-chunk segments were chosen (1080p: 2 700 workgroups; 1/4 of 4K: 2 700) 2-chunk ones (4 050) were
+// faster (1080p flat 31.6k -> 34.3k fps, 4K part 1/4 38.7k -> 40.8k); elsewhere the choice is unchanged.
 constexpr uint64_t kMinFragBlocks = 2000;   // measured best or near-best for 4K at 1, 2, 4, 8 row-band parts and 1080p
 static uint32_t g_segch = kSegChunks;
 
 void fragment_configure(uint32_t W, uint32_t rows_local) {
     static const uint64_t min_blocks = getenv("S3R_MIN_BLOCKS") ? strtoull(getenv("S3R_MIN_BLOCKS"), nullptr, 10)
                                                                 : kMinFragBlocks;   // tuning override
+    static const bool try3 = getenv("S3R_SEG3") != nullptr;                        // tuning override
     g_segch = 1;
     for (uint32_t c : {6u, 3u, 2u}) {
+        if (c == 3u && !try3) continue;
         const uint64_t blocks = (uint64_t)((rows_local + kWaves - 1) / kWaves) * ((W + kChunk * c - 1) / (kChunk * c));
         if (blocks >= min_blocks) { g_segch = c; break; }
     }
