@@ -1285,12 +1285,30 @@ struct alignas(16) RasterRec {                     // 64 B: one line per live sl
 };
 static_assert(sizeof(RasterRec) == 64, "RasterRec layout");
 
+// The corner's camera-space and raster position (render.cpp:286, :288).  The two projections share
+// one refined reciprocal of -cv.z where the trimmed division is exact (div_in_range, s3r_common.h);
+// z = (0 * factor) / nz + nz is nz itself unless nz == 0 (0 / 0: the reference's NaN).
 __device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint32_t vi, const Mat34 &m, float factor,
                                             float half_w, float half_h, Vert &d) {
     const F3 c = mat_mul(m, vtx[vi]);                                     // :286
     const float nz = -c.z;
     d.cv = c;
-    d.rv = mk3((c.x * factor) / nz + half_w, ((-c.y) * factor) / nz + half_h, (0.0f * factor) / nz + nz);   // :288
+    const float px = c.x * factor, py = (-c.y) * factor;
+    float qx, qy;
+#ifndef S3R_TRIM_PROJ
+#define S3R_TRIM_PROJ 1
+#endif
+    if (S3R_TRIM_PROJ && (div_in_range(px, nz) & div_in_range(py, nz))) {
+        const float r = div_recip(nz);
+        qx = div_with_recip(px, nz, r);
+        qy = div_with_recip(py, nz, r);
+    } else {
+        qx = px / nz;
+        qy = py / nz;
+    }
+    float rz = nz;                                                          // (+-0) + nz == nz
+    if (nz == 0.0f) rz = (0.0f * factor) / nz + nz;
+    d.rv = mk3(qx + half_w, qy + half_h, rz);                               // :288
 }
 
 // Local rows [lo, hi] of this rank that fall in frame rows [ymin, ymax] (interleaved bands: local

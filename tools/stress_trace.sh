@@ -1,12 +1,13 @@
 #!/bin/bash
 # rocprofv3 kernel stats of the stress scene (tile path) at 3840x2160, part 0 of N (N = 1 and 8),
-# into $1/n<N>/ (run on the GPU box; the scene is cached in /tmp/s3r_stress.bin).
+# into $1/n<N>/ (run on the GPU box; the scene is cached in /tmp/s3r_stress.bin).  S3R_SERIAL=1 (default
+# here): frames do not overlap, so each kernel is timed alone.
 set -o pipefail
 OUT=${1:-gpurun_out/stress_trace}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 for n in 1 8; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/n$n" -o run --output-format csv -- \
+  S3R_SERIAL=${S3R_SERIAL:-1} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/n$n" -o run --output-format csv -- \
     python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data /tmp/s3r_stress.bin --nparts $n --steps 20 \
     > "$OUT/n$n.log" 2>&1 || exit 1
   python3 - "$OUT/n$n" <<'PY'
