@@ -748,7 +748,11 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     const float lvy = div_with_recip(ooz, dvy, div_recip(dvy));
     // out-of-range texture index: UB in the reference, 0 here and in the oracle (texel())
     const bool tex_ok = texd & (tex_base < ntex) & (ntex - tex_base >= kTexTexels);
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 256)
+    uint32_t rgb = (tex_ok ? tex_base + texel_offset(mu, mv, lvx, lvy) : 0u) * 0x010101u;   // ablation: no load
+#else
     uint32_t rgb = tex[tex_ok ? tex_base + texel_offset(mu, mv, lvx, lvy) : 0u];
+#endif
     auto norm = [&ok](F3 v) {
         const float d = dot3(v, v);
         ok &= sqrt_in_range_ok(d);
