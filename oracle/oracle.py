@@ -39,6 +39,8 @@ def lib():
         _lib.oracle_factor.restype = ctypes.c_float
         _lib.oracle_repeat_add.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_uint32]
         _lib.oracle_repeat_add.restype = ctypes.c_float
+        _lib.oracle_set_row_windows.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
+        _lib.oracle_set_row_windows.restype = ctypes.c_int
     return _lib
 
 
@@ -58,6 +60,13 @@ class OracleRenderer:
         i = Input.of(inp)
         lib().oracle_updateAndRender(ctypes.byref(pd), ctypes.byref(i))
         return out
+
+    def set_row_windows(self, windows):
+        """Rasterise only rows in the [y0, y1) windows (others are walked, not drawn; [] = all rows):
+        a test extension for checking full-size frames on a few rows (render_oracle.c)."""
+        flat = (ctypes.c_uint32 * max(1, 2 * len(windows)))(*[v for w in windows for v in w])
+        if lib().oracle_set_row_windows(flat, len(windows)) != 0:
+            raise ValueError('at most 16 row windows')
 
     def camera_matrix(self) -> np.ndarray:
         m = (ctypes.c_float * 12)()

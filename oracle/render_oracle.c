@@ -304,6 +304,19 @@ static void clip(data_t *data, uint64_t *v_count, uint64_t *a_count, uint64_t *v
     }
 }
 
+/* Test extension (not in the reference): with row windows set, rows outside every window are still
+ * walked -- wy += dy once per row (render.cpp:378), exactly as the loop below does -- but not
+ * rasterised, so a full-size frame (the 20 M-triangle stress scene) can be checked on a few rows in
+ * seconds.  A row's pixels depend only on its walk state, so the windows' rows are the reference's. */
+#define ORACLE_MAX_WINDOWS 16
+static uint32_t win_count = 0, win_rows[2 * ORACLE_MAX_WINDOWS];
+static int row_in_windows(uint32_t y) {
+    if (!win_count) return 1;
+    for (uint32_t i = 0; i < win_count; i++)
+        if (y >= win_rows[2 * i] && y < win_rows[2 * i + 1]) return 1;
+    return 0;
+}
+
 /* render.cpp:264-384 */
 static void render_frame(const PixelData *pd, const Input *in) {
     if (!initialized) {
@@ -393,6 +406,13 @@ static void render_frame(const PixelData *pd, const Input *in) {
             tpp = add2(add2(mul2(uv[0], v2(dx.x, dy.x)), mul2(uv[1], v2(dx.y, dy.y))), mul2(uv[2], v2(dx.z, dy.z)));
         }
         for (uint32_t y = ymin; y <= ymax; y++) {                          /* :360-382 */
+            if (!row_in_windows(y)) {                                      /* (test extension) */
+                pb += xmax - xmin + 1; db += xmax - xmin + 1;
+                wy = add3(wy, dy);
+                w = wy;
+                pb += xdelta; db += xdelta;
+                continue;
+            }
             for (uint32_t x = xmin; x <= xmax; x++) {
                 if (w.x >= 0 && w.y >= 0 && w.z >= 0) {
                     const float ooz = dot3(rvz, w);
@@ -438,6 +458,7 @@ static void free_scene(void) {
 /* ---------------- exported oracle interface (test infrastructure) ---------------- */
 void oracle_set_data_path(const char *path) {
     free_scene();
+    win_count = 0;
     initialized = 0;
     reset_state();
     strncpy(data_path, path, sizeof data_path - 1);
@@ -448,6 +469,14 @@ void oracle_set_data_path(const char *path) {
 void oracle_updateAndRender(const PixelData *pixel_data, const Input *input) {
     if (cfg_scale == 0) reset_state();
     render_frame(pixel_data, input);
+}
+
+/* Row windows [rows[2i], rows[2i+1]), i < n (n <= 16; n = 0: every row) -- see row_in_windows. */
+int oracle_set_row_windows(const uint32_t *rows, uint32_t n) {
+    if (n > ORACLE_MAX_WINDOWS) return -1;
+    for (uint32_t i = 0; i < 2 * n; i++) win_rows[i] = rows[i];
+    win_count = n;
+    return 0;
 }
 
 /* Debug view of the camera matrix (rows), for host-logic tests. */

@@ -40,6 +40,9 @@ CASES = [
     ('regular', 'P_floor', 1280, 720),
     ('full', 'P_over', 1000, 333),     # width not a multiple of the 512-pixel segment
     ('full', 'P_id', 17, 5),           # tiny frame
+    ('full', 'P_over', 3840, 2160),    # BASELINE config 3 (the bench workload)
+    ('full', 'P_id', 3840, 2160),
+    ('full', 'P_over', 7680, 4320),    # BASELINE config 4's frame, whole on one GPU
 ]
 
 

@@ -93,3 +93,24 @@ def test_repeat_add_is_sequential():
     for _ in range(777):
         want = np.float32(want + d)
     assert np.float32(repeat_add(float(s), float(d), 777)) == want
+
+
+@pytest.mark.parametrize('scene_name,pose', [('full', 'P_over'), ('full', 'P_clip')])
+def test_row_windows_equal_full_frame_rows(scene_dir, scene_name, pose):
+    """The oracle's row-window mode (rows outside the windows walked, not drawn) gives the full
+    frame's pixels on the window rows and the background elsewhere."""
+    from oracle.oracle import OracleRenderer
+    W, H = 320, 240
+    full = render_pose(scene_dir[scene_name], poses.script(pose), W, H)
+    r = OracleRenderer(scene_dir[scene_name])
+    wins = [(0, 9), (100, 117), (239, 240)]
+    r.set_row_windows(wins)
+    out = None
+    for t in poses.script(pose):
+        out = r.update_and_render(W, H, t)
+    mask = np.zeros(H, dtype=bool)
+    for a, b in wins:
+        mask[a:b] = True
+    assert np.array_equal(out[mask], full[mask])
+    assert (out[~mask] == 0x1E1E1E).all()
+    assert (full[mask] != 0x1E1E1E).any()

@@ -79,6 +79,34 @@ def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir):
     assert np.array_equal(got, want), diff(got, want)
 
 
+def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
+    """BASELINE config 5 at full size: 1 000 000 icosahedra (20 M triangles) at 3840x2160.  The GPU
+    frame is whole; the oracle draws only a few row windows (every other row is walked, not drawn --
+    oracle_set_row_windows), and those rows must match bit for bit."""
+    from oracle.oracle import OracleRenderer
+    path = str(tmp_path / 'icosa-stress.bin')
+    stress.write_named('icosa-stress', path)
+    W, H = 3840, 2160
+    inp = poses.script('P_id')[-1]
+    got = gpu_renderer_frame(gpu_renderer, path, W, H, inp)
+    wins = [(0, 16), (700, 716), (1079, 1097), (2144, 2160)]
+    o = OracleRenderer(path)
+    o.set_row_windows(wins)
+    want = o.update_and_render(W, H, inp)
+    o.reset(path)                                   # frees the 4 GB scene, clears the windows
+    rows = np.concatenate([np.arange(a, b) for a, b in wins])
+    assert (want[rows] != 0x1E1E1E).mean() > 0.5     # the windows see icosahedra
+    assert np.array_equal(got[rows], want[rows]), diff(got[rows], want[rows])
+
+
+def gpu_renderer_frame(r, path, W, H, inp):
+    r.configure(path)
+    try:
+        return r.update_and_render(W, H, inp)
+    finally:
+        r.configure(None)                           # drop the 4 GB scene; back to the packaged data.bin
+
+
 @pytest.mark.parametrize('band,nparts', [(16, 2), (16, 3), (5, 2), (7, 4)])
 def test_tile_bands_reassemble(gpu_renderer, icosa_dir, band, nparts):
     """Row bands rendered separately on the tile path == the whole frame (multi-GPU exactness)."""
