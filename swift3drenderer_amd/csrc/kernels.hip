@@ -935,6 +935,9 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 // them kTPB at a time: its lanes first act as (triangle, barycentric component) pairs and advance
 // that component's exact walk (render.cpp:374) to the chunk, publishing (value, step) in LDS; then
 // its lanes act as pixels: edge test, 1/z, strict '>' depth test in registers; the winner is shaded.
+#ifndef S3R_WATERFALL_MIN
+#define S3R_WATERFALL_MIN 6            // segment chunks from which the shading takes the waterfall
+#endif
 template <uint32_t SEGCH>
 __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
@@ -1229,11 +1232,40 @@ __global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetu
             if (row_ok && xp <= xe)
                 row[xp] = win[p] < 0 ? kBackground : (uint32_t)win[p] ^ __float_as_uint(bw0[p] + bw1[p] + bw2[p] + depth[p]);
 #else
+#if defined(S3R_ABLATE) && (S3R_ABLATE & 512)
             if (row_ok && xp <= xe)
+#endif
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 512)     // ablation: every shade reads one record
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #else
-                row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+            if (SEGCH < S3R_WATERFALL_MIN) {
+                if (row_ok && xp <= xe)
+                    row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+            } else {
+                // waterfall over the wave's distinct winners (usually one: a chunk inside one
+                // triangle): each round shades the lanes of one winner, whose record address is
+                // wave-uniform, so its constants arrive by scalar loads into SGPRs -- no per-lane
+                // gather, and ~36 VGPRs fewer live at the shading's peak
+                const int wp = win[p];
+                const bool act = row_ok && xp <= xe;
+                uint32_t px = kBackground;
+                uint64_t todo = __ballot(act && wp >= 0);
+                while (todo) {
+                    const int wu = __builtin_amdgcn_readlane(wp, (int)__builtin_ctzll(todo));
+                    // loaded in wave-uniform control flow: scalar loads
+                    const TriSetup *tp = tris + wu;
+                    const float4 *q = reinterpret_cast<const float4 *>(tp);
+                    const float4 c0 = q[6], c1 = q[7], c2 = q[8], n0 = q[9], n1 = q[10], n2 = q[11];
+                    const float4 k0 = q[12], k1 = q[13], k2 = q[14];
+                    const uint32_t kind = tp->kind, tex_base = tp->tex_base;
+                    const bool mine = act && wp == wu;
+                    todo &= ~__ballot(mine);
+                    if (mine)
+                        px = shade_core_flat(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
+                                             depth[p], tex, ntex);
+                }
+                if (act) row[xp] = px;
+            }
 #endif
 #endif
         }
@@ -1958,9 +1990,9 @@ constexpr uint64_t kMinFragBlocks = 2000;   // measured best or near-best for 4K
 static uint32_t g_segch = kSegChunks;
 
 void fragment_configure(uint32_t W, uint32_t rows_local) {
-    static const uint64_t min_blocks = getenv("S3R_MIN_BLOCKS") ? strtoull(getenv("S3R_MIN_BLOCKS"), nullptr, 10)
-                                                                : kMinFragBlocks;   // tuning override
-    static const bool try3 = getenv("S3R_SEG3") != nullptr;                        // tuning override
+    const char *mb_env = getenv("S3R_MIN_BLOCKS");                                  // tuning / test override
+    const uint64_t min_blocks = mb_env ? strtoull(mb_env, nullptr, 10) : kMinFragBlocks;
+    const bool try3 = getenv("S3R_SEG3") != nullptr;                                // tuning override
     g_segch = 1;
     for (uint32_t c : {6u, 3u, 2u}) {
         if (c == 3u && !try3) continue;
