@@ -938,8 +938,11 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 #ifndef S3R_WATERFALL_MIN
 #define S3R_WATERFALL_MIN 6            // segment chunks from which the shading takes the waterfall
 #endif
+#ifndef S3R_OCC_WIDE
+#define S3R_OCC_WIDE 6                 // waterfall-shading instances: <= 80 VGPRs (79 used, no spills);
+#endif                                 // 7 (72 VGPRs, 8 tables for the LDS) spills and is 5 % slower
 template <uint32_t SEGCH>
-__global__ void __launch_bounds__(64 * kWaves, S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
+__global__ void __launch_bounds__(64 * kWaves, SEGCH >= S3R_WATERFALL_MIN ? S3R_OCC_WIDE : S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
