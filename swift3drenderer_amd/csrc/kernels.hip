@@ -935,14 +935,18 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 // them kTPB at a time: its lanes first act as (triangle, barycentric component) pairs and advance
 // that component's exact walk (render.cpp:374) to the chunk, publishing (value, step) in LDS; then
 // its lanes act as pixels: edge test, 1/z, strict '>' depth test in registers; the winner is shaded.
-#ifndef S3R_WATERFALL_MIN
-#define S3R_WATERFALL_MIN 6            // segment chunks from which the shading takes the waterfall
+#ifndef S3R_WATERFALL_BINS
+#define S3R_WATERFALL_BINS 4000        // launches of >= this many 384-px bins shade by the waterfall
 #endif
 #ifndef S3R_OCC_WIDE
 #define S3R_OCC_WIDE 6                 // waterfall-shading instances: <= 80 VGPRs (79 used, no spills);
 #endif                                 // 7 (72 VGPRs, 8 tables for the LDS) spills and is 5 % slower
-template <uint32_t SEGCH>
-__global__ void __launch_bounds__(64 * kWaves, SEGCH >= S3R_WATERFALL_MIN ? S3R_OCC_WIDE : S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
+// WF: shading by the waterfall over the wave's distinct winners, each winner's constants by scalar
+// loads (79 VGPRs: occupancy 6).  It pays where the launch is throughput-bound (4K, 8K frames: +1.5 %,
+// +3.7 %); launches of one or two rounds of workgroups are bound by their heaviest bins' latency,
+// which the extra waterfall rounds lengthen (a 4K frame half: -4 %, 1080p: -4 %).
+template <uint32_t SEGCH, bool WF>
+__global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
@@ -1241,7 +1245,7 @@ __global__ void __launch_bounds__(64 * kWaves, SEGCH >= S3R_WATERFALL_MIN ? S3R_
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 512)     // ablation: every shade reads one record
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #else
-            if (SEGCH < S3R_WATERFALL_MIN) {
+            if (!WF) {
                 if (row_ok && xp <= xe)
                     row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
             } else {
@@ -2040,7 +2044,10 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
         if (done) (void)hipEventRecord(done, st);
         return;
     }
-    auto kern = g_segch == 6 ? k_fragment<6> : g_segch == 3 ? k_fragment<3> : g_segch == 2 ? k_fragment<2> : k_fragment<1>;
+    const char *wf_env = getenv("S3R_WATERFALL_BINS");                             // tuning / test override
+    const uint64_t wf_bins = wf_env ? strtoull(wf_env, nullptr, 10) : S3R_WATERFALL_BINS;
+    auto kern = g_segch == 6 ? (blocks >= wf_bins ? k_fragment<6, true> : k_fragment<6, false>)
+              : g_segch == 3 ? k_fragment<3, false> : g_segch == 2 ? k_fragment<2, false> : k_fragment<1, false>;
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs, tag,

@@ -266,11 +266,14 @@ def test_longest_first_order(gpu_renderer, scene_dir, monkeypatch):
 @pytest.mark.parametrize('scene_name,pose,w,h', [('full', 'P_over', 640, 480), ('full', 'P_clip', 640, 480),
                                                  ('flat', 'P_over', 640, 480), ('tetra', 'P_tetra', 640, 480),
                                                  ('regular', 'P_floor', 1280, 720), ('full', 'P_id', 1000, 333)])
-def test_widest_segments_match_oracle(gpu_renderer, scene_dir, monkeypatch, scene_name, pose, w, h):
+@pytest.mark.parametrize('waterfall', [False, True])
+def test_widest_segments_match_oracle(gpu_renderer, scene_dir, monkeypatch, scene_name, pose, w, h, waterfall):
     """Small frames forced onto the widest fragment segments (S3R_MIN_BLOCKS=1: 384-pixel segments,
-    the launch shape of 4K and 8K frames, whose shading takes the waterfall over the wave's
-    distinct winners): every frame equals the oracle's."""
+    the launch shape of 4K and 8K frames), with the shading by per-lane gathers or by the waterfall
+    over the wave's distinct winners (S3R_WATERFALL_BINS=0: the 4K / 8K instance): every frame equals
+    the oracle's."""
     monkeypatch.setenv('S3R_MIN_BLOCKS', '1')
+    monkeypatch.setenv('S3R_WATERFALL_BINS', '0' if waterfall else '1000000000')
     path = scene_dir[scene_name]
     script = poses.script(pose)
     want = oracle_render_pose(path, script, w, h, extra_frames=1)
