@@ -211,6 +211,7 @@ def main():
         for _ in range(3):
             delivered(hold)
         e2e_multi = kg / timed(delivered, kg)
+        r.unregister_host(hf.frame)            # before the mapping goes away
         hf.close()
 
     fps = a.steps / el

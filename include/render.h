@@ -81,11 +81,17 @@ int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height, ui
  * frame rows of a caller-owned HOST frame (width x height u32, row-major), asynchronously on `stream`:
  * one rectangular copy over this GPU's own PCIe link (the part's bands are band_rows x width blocks
  * spaced n_parts bands apart) plus one for a trailing partial band.  The host frame is page-locked
- * on first use (cached per pointer and size, dropped on resize and shutdown).  N GPUs -- one process
+ * on first use (cached per pointer and size, dropped on resize and shutdown, or by
+ * s3r_unregister_host -- call it before unmapping or freeing the frame).  N GPUs -- one process
  * each, the frame in shared memory -- fill one host frame over N links in parallel.  Returns the rows
  * copied, or -1 on bad arguments. */
 int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t height, uint32_t band_rows,
                           uint32_t n_parts, uint32_t part, uint32_t *host_frame, void *stream);
+
+/* Drop the library's page-lock of a caller host buffer starting at ptr (waits for the device first);
+ * a no-op for a pointer the library never registered.  For host frames about to be unmapped or freed
+ * (updateAndRender buffers need not: a stale registration is detected and replaced there). */
+void s3r_unregister_host(void *ptr);
 
 /* Rows of a height-row frame owned by `part`. */
 uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);

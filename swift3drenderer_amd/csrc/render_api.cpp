@@ -772,6 +772,19 @@ __attribute__((visibility("default"))) int64_t s3r_bands_to_host(const uint32_t 
     return rows;
 }
 
+__attribute__((visibility("default"))) void s3r_unregister_host(void *ptr) {
+    if (!ptr) return;
+    for (size_t i = g.regs.size(); i-- > 0;) {
+        if (g.regs[i].p != ptr) continue;
+        if (g.regs[i].ok) {
+            if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
+            HIPCHECK(hipDeviceSynchronize());          // no copy into it may still be in flight
+            (void)hipHostUnregister(ptr);
+        }
+        g.regs.erase(g.regs.begin() + (long)i);
+    }
+}
+
 __attribute__((visibility("default"))) void s3r_timing(int enable) {
     g.timing = enable != 0;
     g.tcount = 0;

@@ -16,7 +16,7 @@ from .abi import Input, pixel_data_for
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 
-EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_set_raster_path', 's3r_raster_path',
+EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host',
            's3r_render_bands', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
 
 _lib = None
@@ -54,6 +54,8 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_bands_to_host.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     lib.s3r_bands_to_host.restype = ctypes.c_int64
+    lib.s3r_unregister_host.argtypes = [ctypes.c_void_p]
+    lib.s3r_unregister_host.restype = None
     lib.s3r_debug_set_frame_count.argtypes = [ctypes.c_uint32]
     lib.s3r_debug_set_frame_count.restype = None
     _lib = lib
@@ -119,6 +121,10 @@ class Renderer:
         if r < 0:
             raise ValueError('s3r_bands_to_host: bad arguments')
         return int(r)
+
+    def unregister_host(self, host: np.ndarray):
+        """Drop the page-lock bands_to_host took on `host` (before the array is freed / unmapped)."""
+        self.lib.s3r_unregister_host(ctypes.c_void_p(host.ctypes.data))
 
     def set_raster_path(self, mode: str | int):
         """'auto' | 'rows' | 'tiles' (or 0/1/2): the fragment-stage strategy, include/render.h."""

@@ -187,6 +187,7 @@ def test_gpu_bands_to_host_frame(gpu_renderer, scene_dir, W, H, nparts, band):
         assert r.bands_to_host(buf.data_ptr(), W, H, band, nparts, p, host, st) == rows
         bufs.append(buf)
     torch.cuda.synchronize()
+    r.unregister_host(host)
     if not np.array_equal(host, want):
         ys, xs = np.nonzero(host != want)
         raise AssertionError(f'{len(ys)} pixels differ; first at (x={xs[0]}, y={ys[0]}): host {host[ys[0], xs[0]]:#x} '
