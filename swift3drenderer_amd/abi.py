@@ -26,7 +26,9 @@ class Input(ctypes.Structure):
 
     @classmethod
     def of(cls, t):
-        """Build from an (up, down, left, right, mouse.x, mouse.y) tuple."""
+        """Build from an (up, down, left, right, mouse.x, mouse.y) tuple (an Input passes through)."""
+        if isinstance(t, cls):
+            return t
         return cls(*(float(v) for v in t))
 
 

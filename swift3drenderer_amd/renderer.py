@@ -42,7 +42,7 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_set_raster_path.restype = ctypes.c_int
     lib.s3r_raster_path.argtypes = []
     lib.s3r_raster_path.restype = ctypes.c_int
-    lib.s3r_render_bands.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+    lib.s3r_render_bands.argtypes = [ctypes.POINTER(Input), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     lib.s3r_render_bands.restype = ctypes.c_int64
     lib.s3r_band_rows_local.argtypes = [ctypes.c_uint32] * 4
@@ -103,9 +103,7 @@ class Renderer:
                      stream: int = 0) -> int:
         """Render one part of an interleaved row-band split into device memory at dev_ptr, on the
         HIP stream `stream` (0 = the default stream, i.e. torch's default stream)."""
-        i = Input.of(inp)
-        r = self.lib.s3r_render_bands(ctypes.byref(i), width, height, band, nparts, part,
-                                      ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None))
+        r = self.lib.s3r_render_bands(Input.of(inp), width, height, band, nparts, part, dev_ptr, stream or None)
         if r < 0:
             raise ValueError('s3r_render_bands: bad arguments')
         return int(r)

@@ -39,7 +39,8 @@ def main():
     N, B = a.nparts, (a.band if a.nparts > 1 else H)
     buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
     sptr = torch.cuda.current_stream().cuda_stream
-    script, hold = poses.script(a.pose), poses.hold(a.pose)
+    from swift3drenderer_amd.abi import Input
+    script, hold = poses.script(a.pose), Input.of(poses.hold(a.pose))   # built once, as bench.py does
     for t in script:
         r.render_bands(t, W, H, B, N, 0, buf.data_ptr(), sptr)
     for _ in range(50):
