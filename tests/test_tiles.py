@@ -86,10 +86,22 @@ def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
     from oracle.oracle import OracleRenderer
     path = str(tmp_path / 'icosa-stress.bin')
     stress.write_named('icosa-stress', path)
+    import torch
     W, H = 3840, 2160
     inp = poses.script('P_id')[-1]
-    got = gpu_renderer_frame(gpu_renderer, path, W, H, inp)
-    wins = [(0, 16), (700, 716), (1079, 1097), (2144, 2160)]
+    r = gpu_renderer
+    r.configure(path)
+    try:
+        got = r.update_and_render(W, H, inp)
+        # one rank's share of an 8-GPU split (part 3, 16-row bands: frame rows 48-63, 176-191, ...)
+        part_rows = r.lib.s3r_band_rows_local(H, 16, 8, 3)
+        buf = torch.empty((part_rows, W), dtype=torch.int32, device='cuda')
+        r.render_bands(inp, W, H, 16, 8, 3, buf.data_ptr(), 0)
+        torch.cuda.synchronize()
+        part = buf.cpu().numpy().view(np.uint32)
+    finally:
+        r.configure(None)                           # drop the 4 GB scene; back to the packaged data.bin
+    wins = [(0, 16), (48, 64), (700, 716), (1072, 1097), (2144, 2160)]
     o = OracleRenderer(path)
     o.set_row_windows(wins)
     want = o.update_and_render(W, H, inp)
@@ -97,14 +109,10 @@ def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
     rows = np.concatenate([np.arange(a, b) for a, b in wins])
     assert (want[rows] != 0x1E1E1E).mean() > 0.5     # the windows see icosahedra
     assert np.array_equal(got[rows], want[rows]), diff(got[rows], want[rows])
-
-
-def gpu_renderer_frame(r, path, W, H, inp):
-    r.configure(path)
-    try:
-        return r.update_and_render(W, H, inp)
-    finally:
-        r.configure(None)                           # drop the 4 GB scene; back to the packaged data.bin
+    # the part's local rows of frame rows 48-63 and 1072-1087 (bands 3 and 67, both part 3's)
+    for y0 in (48, 1072):
+        lr0 = (y0 // 16 // 8) * 16
+        assert np.array_equal(part[lr0:lr0 + 16], want[y0:y0 + 16]), f'part 3 rows {y0}..{y0 + 15}'
 
 
 @pytest.mark.parametrize('band,nparts', [(16, 2), (16, 3), (5, 2), (7, 4)])
