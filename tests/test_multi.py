@@ -192,3 +192,39 @@ def test_gpu_bands_to_host_frame(gpu_renderer, scene_dir, W, H, nparts, band):
         ys, xs = np.nonzero(host != want)
         raise AssertionError(f'{len(ys)} pixels differ; first at (x={xs[0]}, y={ys[0]}): host {host[ys[0], xs[0]]:#x} '
                              f'oracle {want[ys[0], xs[0]]:#x}')
+
+
+@pytest.mark.gpu
+def test_gpu_bands_to_host_after_unregister(gpu_renderer, scene_dir):
+    """bands_to_host into a host frame, s3r_unregister_host, the frame freed and a new one of the
+    same size allocated (often at the same address): the new frame receives the next delivery."""
+    from oracle.oracle import render_pose as oracle_render_pose
+    from swift3drenderer_amd import poses
+    r = gpu_renderer
+    W, H, N, band = 640, 480, 2, 16
+    dev = torch.device('cuda', 0)
+    script = poses.script('P_over')
+    want = oracle_render_pose(scene_dir['full'], script, W, H)
+    r.configure(scene_dir['full'])
+    st = torch.cuda.current_stream(dev).cuda_stream
+    scratch = torch.empty((H, W), dtype=torch.int32, device=dev)
+    for t in script:
+        r.render_bands(t, W, H, H, 1, 0, scratch.data_ptr(), st)
+    hold = poses.hold('P_over')
+    bufs = [torch.empty((band_rows(H, band, N, p), W), dtype=torch.int32, device=dev) for p in range(N)]
+    same = 0
+    host = np.zeros((H, W), dtype=np.uint32)
+    for rep in range(3):
+        if rep:
+            addr = host.ctypes.data
+            r.unregister_host(host)
+            del host
+            host = np.zeros((H, W), dtype=np.uint32)
+            same += host.ctypes.data == addr
+        for p in range(N):
+            r.render_bands(hold, W, H, band, N, p, bufs[p].data_ptr(), st)
+            r.bands_to_host(bufs[p].data_ptr(), W, H, band, N, p, host, st)
+        torch.cuda.synchronize()
+        assert np.array_equal(host, want), f'delivery {rep}'
+    r.unregister_host(host)
+    print(f'new frame at the old address {same} of 2 times')
