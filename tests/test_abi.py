@@ -97,3 +97,15 @@ def test_render_bands_rejects_bad_arguments():
     i = abi.Input()
     assert lib.s3r_render_bands(ctypes.byref(i), 16, 16, 0, 1, 0, None, None) == -1
     assert lib.s3r_render_bands(ctypes.byref(i), 16, 16, 4, 2, 2, None, None) == -1
+    # an Input instance passes straight through (POINTER(Input) argtype, Input.of identity)
+    assert abi.Input.of(i) is i
+    assert lib.s3r_render_bands(i, 16, 16, 0, 1, 0, None, None) == -1
+
+
+def test_unregister_host_is_a_no_op_for_unknown_pointers():
+    """s3r_unregister_host on NULL or on memory the library never page-locked touches no device."""
+    import numpy as np
+    lib = load_library()
+    lib.s3r_unregister_host(None)
+    a = np.zeros(16, dtype=np.uint32)
+    lib.s3r_unregister_host(ctypes.c_void_p(a.ctypes.data))
