@@ -237,8 +237,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #endif
 
 // Timing build (-DS3R_WGTIME, tools/wg_timeline.py): per-workgroup phase timestamps of k_fragment.
-constexpr uint32_t kWgTimesMax = 65536;
 #ifdef S3R_WGTIME
+constexpr uint32_t kWgTimesMax = 65536;
 // slots 0-3: wave 0's 100 MHz wall clock at start, list loaded, walk state loaded, end; 4-6: wave 0's
 // shader-clock cycles summed over its chunks in batch 0, later batches, shading + stores; 7: list length;
 // 8-10: wave 0's chunks whose batch 0 took the slow (walk + linear_run) path, had a non-linear
