@@ -1,15 +1,23 @@
 #!/usr/bin/env python3
-"""Benchmark: frames/s and Mpixels/s of updateAndRender's frame at 3840x2160 on the packaged scene.
+"""Benchmark: frames/s and Mpixels/s of updateAndRender at 3840x2160 on the packaged scene
+(BASELINE.json metric).
 
-Step = one frame of the hot path (render.cpp:264-384): camera update, vertex transform, triangle
-setup/clip/cull, fragment stage, with the frame left in device memory (HBM-resident value; the
-PCIe-inclusive updateAndRender rate is reported separately as `e2e_fps_with_d2h`).  With N GPUs
-the frame's rows are split into interleaved bands (band g -> rank g % N) and every rank renders its
-bands into its own HBM: `value` counts frames whose rows are all rendered, left where they were
-rendered, as the one-GPU frame is left in its GPU's HBM.  Reassembling every frame on rank 0 with
-one RCCL gather over xGMI (torch.distributed, nccl backend) is timed in a second loop and reported
-as `gathered_fps`; the frame is then 33 MB per 4K frame moving over xGMI, and that loop is bound by
-rank 0's xGMI ingest, not by rendering (multi-GPU).
+A step is one call of the reference's boundary, ``updateAndRender(PixelData*, Input*)``
+(render.cpp:264-384): camera update, geometry, fragment stage, and the finished frame in the
+caller's HOST buffer when the call returns -- timed the way the reference's main loop times it
+(main.swift:120-122), one call at a time, into a caller-owned buffer allocated the way main.swift
+allocates it: ONE malloc of 2 * bufferSize whose halves are used alternately (main.swift:117-118,
+:164).  ``value`` = 1 / the median wall time of those calls, over at least 200 timed frames
+(whatever --steps says; the count used is reported in ``steps``) after at least 20 warm-up frames.
+
+N GPUs: the reference's caller is one process on one thread, so the N GPUs sit behind that one call
+(s3r_configure_devices): rank 0 calls updateAndRender with devices 0..N-1, each rendering its
+interleaved 16-row bands and copying them into their rows of the caller's buffer over its own PCIe
+link.  Ranks 1..N-1 only take part in the barriers (gloo).  Scaling is strong (a fixed frame).
+
+Beside ``value``: ``device_fps`` (one GPU, frames pipelined and left in HBM: s3r_render_bands),
+the ``roofline`` of the fragment kernel (HIP events on its stream during updateAndRender frames),
+and ``cpu_baseline`` (the single-threaded CPU oracle on this host, a bounded sample).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -17,6 +25,7 @@ rank 0's xGMI ingest, not by rendering (multi-GPU).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -32,23 +41,26 @@ METRIC = 'frames/sec + Mpixels/s at 3840x2160, data.bin scene; 1/2/4/8-GPU scali
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md, HBM3E peak (spec)
 TRI_SETUP_BYTES = 240    # sizeof(TriSetup)
 RASTER_REC_BYTES = 64    # sizeof(RasterRec), tile path
+MIN_TIMED = 200          # >= 200 frames after 20 warm-up frames
+MIN_WARMUP = 20
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=200)
-    p.add_argument('--warmup', type=int, default=20)
+    p.add_argument('--steps', type=int, default=MIN_TIMED)
+    p.add_argument('--warmup', type=int, default=MIN_WARMUP)
     p.add_argument('--width', type=int, default=3840)
     p.add_argument('--height', type=int, default=2160)
     p.add_argument('--scene', default='full')
     p.add_argument('--pose', default='P_over')
     p.add_argument('--band', type=int, default=16, help='rows per interleaved band (multi-GPU)')
+    p.add_argument('--devices', default=None,
+                   help='comma-separated device ids behind updateAndRender (default 0..N-1; ids may repeat '
+                        'to rehearse N parts on one GPU)')
     p.add_argument('--cpu-seconds', type=float, default=10.0, help='CPU-baseline sample budget')
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--no-e2e', action='store_true')
-    p.add_argument('--backend', default='nccl', help="torch.distributed backend: nccl (RCCL) or gloo "
-                   "(rehearsal only: gathers through host memory)")
+    p.add_argument('--no-device', action='store_true', help='skip the device-resident (HBM) rate')
     return p.parse_args()
 
 
@@ -92,6 +104,37 @@ def load_traffic(workload_key):
         return None
 
 
+class DoubleBuffer:
+    """main.swift:117-118, :164: one malloc of 2 * bufferSize, halves used alternately."""
+
+    def __init__(self, w, h):
+        import numpy as np
+        from swift3drenderer_amd.abi import PixelData
+        self.libc = ctypes.CDLL(None)
+        self.libc.malloc.restype = ctypes.c_void_p
+        self.libc.malloc.argtypes = [ctypes.c_size_t]
+        self.libc.free.argtypes = [ctypes.c_void_p]
+        self.size = 4 * w * h
+        self.ptr = self.libc.malloc(2 * self.size)
+        if not self.ptr:
+            raise MemoryError('malloc of the double buffer failed')
+        self.halves = [PixelData(ctypes.cast(self.ptr + k * self.size, ctypes.POINTER(ctypes.c_uint32)), w, h, 4,
+                                 self.size) for k in (0, 1)]
+        self.cur = 0
+        self.np = np
+
+    def next(self):
+        pd = self.halves[self.cur]
+        self.cur ^= 1
+        return pd
+
+    def half(self, k):
+        return (ctypes.c_uint8 * self.size).from_address(self.ptr + k * self.size)
+
+    def free(self):
+        self.libc.free(self.ptr)
+
+
 def main():
     a = parse()
     import numpy as np
@@ -100,196 +143,176 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit('--gpus N>1 needs torch.distributed.run with N processes')
-    # one process per GPU; on a box with fewer GPUs than ranks (a gloo rehearsal) ranks share them
-    local = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    if world == 1 and a.gpus > 1:
+        raise SystemExit('--gpus N>1 needs torch.distributed.run with N processes')
+    N = max(world, 1)
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        if a.backend == 'nccl':
-            dist.init_process_group('nccl', device_id=dev)
-        else:
-            dist.init_process_group(a.backend)
+        # control only (barriers, the max over ranks): the frame's data path is inside rank 0's call
+        dist.init_process_group('gloo')
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    result = None
+    if rank == 0:
+        result = run_rank0(a, N, np, torch)
+        print(json.dumps(result), flush=True)
+    barrier()
+    if world > 1:
+        dist.destroy_process_group()
+    return result
+
+
+def run_rank0(a, N, np, torch):
     from swift3drenderer_amd import poses, scene
-    from swift3drenderer_amd.multi import BandGather
+    from swift3drenderer_amd.abi import Input
     from swift3drenderer_amd.renderer import Renderer
 
-    tmp = tempfile.mkdtemp(prefix=f's3r_bench_{rank}_')
+    ndev = torch.cuda.device_count()
+    devices = [int(x) for x in a.devices.split(',')] if a.devices else list(range(N))
+    if not a.devices and ndev < N:
+        raise SystemExit(f'--gpus {N}: only {ndev} GPUs visible (use --devices to rehearse parts on one GPU)')
+    tmp = tempfile.mkdtemp(prefix='s3r_bench_')
     data_path = os.path.join(tmp, f'{a.scene}.bin')
     scene.write_named(a.scene, data_path)
-
     W, H, B = a.width, a.height, a.band
-    N = world
     script = poses.script(a.pose)
     hold = poses.hold(a.pose)
-    from swift3drenderer_amd.abi import Input
-    hold_in = Input.of(hold)                 # built once: the timed loops pass it straight through
+    hold_in = Input.of(hold)
+    steps = max(a.steps, MIN_TIMED)
+    warmup = max(a.warmup, MIN_WARMUP)
 
-    r = Renderer(data_path, device=local)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-    rows = r.lib.s3r_band_rows_local(H, B, N, rank) if N > 1 else H
-    local_buf = torch.empty((max(rows, 1), W), dtype=torch.int32, device=dev)
-    if N > 1:
-        # gloo rehearsal (one box, ranks sharing a GPU): the same gather through host memory
-        gdev = dev if a.backend == 'nccl' else torch.device('cpu')
-        bg = BandGather(W, H, B, N, rank, gdev)
+    torch.cuda.set_device(devices[0])
+    dev = torch.device('cuda', devices[0])
+    r = Renderer(data_path, device=devices[0])
+    r.configure_devices(devices if len(devices) > 1 else [], B)
+    r.configure(data_path, devices[0])
+    lib = r.lib
+    buf = DoubleBuffer(W, H)
 
-    def render(inp):
-        """One frame: this rank's rows of the frame into its device buffer (HBM-resident)."""
-        if N == 1:
-            r.render_bands(inp, W, H, H, 1, 0, local_buf.data_ptr(), sptr)
-        elif a.backend == 'nccl':
-            r.render_bands(inp, W, H, B, N, rank, bg.send.data_ptr(), sptr)   # straight into the send buffer
-        else:
-            r.render_bands(inp, W, H, B, N, rank, local_buf.data_ptr(), sptr)
+    def call(inp):
+        lib.updateAndRender(ctypes.byref(buf.next()), ctypes.byref(inp))
 
-    def gathered(inp):
-        """One frame reassembled on rank 0: render, then one gather (RCCL over xGMI)."""
-        render(inp)
-        if a.backend != 'nccl':
-            bg.send[:rows].copy_(local_buf[:rows].cpu())
-        bg.gather()
+    for t in script:                       # the pose script (the first call initialises), untimed
+        call(Input.of(t))
+    for _ in range(warmup):
+        call(hold_in)
 
-    def timed(fn, k):
-        """k frames between barrier + sync pairs; the max over ranks of the elapsed time."""
-        if N > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(k):
-            fn(hold_in)
-        torch.cuda.synchronize(dev)
-        if N > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if N > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == 'nccl' else 'cpu')
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
-
-    for t in script:                     # pose script (first call initialises), untimed
-        render(t)
-    for _ in range(a.warmup):
-        render(hold)
+    # value: synchronous updateAndRender calls, each timed like main.swift:120-122
+    per = np.empty(steps)
+    refs = [ctypes.byref(h) for h in buf.halves]
+    in_ref = ctypes.byref(hold_in)
+    uar = lib.updateAndRender
+    clock = time.perf_counter
     torch.cuda.synchronize(dev)
+    t_start = clock()
+    for k in range(steps):
+        t0 = clock()
+        uar(refs[buf.cur], in_ref)
+        per[k] = clock() - t0
+        buf.cur ^= 1
+    torch.cuda.synchronize(dev)
+    total = clock() - t_start
+    median_s = float(np.median(per))
+    fps = 1.0 / median_s
 
-    # value: frames rendered, each frame's rows left in the HBM of the ranks that own them (N = 1:
-    # the whole frame in one GPU's HBM).  No HIP-event timing inside this loop.
-    el = timed(render, a.steps)
+    # both halves carry the held pose's frame; the pin state the frames were delivered with
+    host = r.host_stats()
+    halves_pinned = [bool(lib.s3r_host_pinned(ctypes.c_void_p(buf.ptr + k * buf.size), buf.size)) for k in (0, 1)]
 
-    # device-side kernel times from HIP events, in a separate pass of the same frames
+    # fragment-kernel time on device 0's stream (HIP events), in a separate pass of the same calls
     r.timing(True)
-    for _ in range(a.steps):
-        render(hold)
+    nt = min(steps, MIN_TIMED)
+    for _ in range(nt):
+        call(hold_in)
     frag_ms, frame_ms, nfr = r.timing_collect()
     r.timing(False)
 
-    # the same frames reassembled on rank 0 by one gather per frame (reported beside value)
-    gathered_fps = None
-    e2e_multi = None
-    if N > 1:
-        for _ in range(3):
-            gathered(hold)
-        kg = max(10, min(100, a.steps))
-        gathered_fps = kg / timed(gathered, kg)
-        # the same frames delivered into ONE host frame shared by the node's ranks (/dev/shm), each
-        # rank copying its own bands over its own GPU's PCIe link (s3r_bands_to_host): the
-        # multi-GPU counterpart of updateAndRender's host buffer
-        from swift3drenderer_amd.multi import HostFrame
-        hf = HostFrame(W, H, rank)
-        src = bg.send if a.backend == 'nccl' else local_buf
-
-        def delivered(inp):
-            render(inp)
-            r.bands_to_host(src.data_ptr(), W, H, B, N, rank, hf.frame, sptr)
-
-        for _ in range(3):
-            delivered(hold)
-        e2e_multi = kg / timed(delivered, kg)
-        r.unregister_host(hf.frame)            # before the mapping goes away
-        hf.close()
-
-    fps = a.steps / el
     counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
     nv, ni, na, ntex, nslots, pairs, path = counts[:7]
+    rows0 = r.lib.s3r_band_rows_local(H, B, len(devices), 0) if len(devices) > 1 and H > B else H
     if path == 2:
         # tile path, fragment stage = k_tile_raster + k_tile_resolve: framebuffer rows, the per-pixel
         # (1/z, slot) keys written and read back, and per (slot, tile) pair its list entry + 64-B record
         kernel = 'k_tile_raster+k_tile_resolve'
-        frag_bytes = 4 * W * rows + 16 * W * rows + (4 + RASTER_REC_BYTES) * pairs
+        frag_bytes = 4 * W * rows0 + 16 * W * rows0 + (4 + RASTER_REC_BYTES) * pairs
     else:
-        # row path, k_fragment: this rank's framebuffer rows + the ripmap texels it may sample + the
+        # row path, k_fragment: device 0's framebuffer rows + the ripmap texels it may sample + the
         # triangle setup records it reads
         kernel = 'k_fragment'
-        frag_bytes = 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
+        frag_bytes = 4 * W * rows0 + 4 * ntex + TRI_SETUP_BYTES * nslots
     frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
     achieved = frag_bytes / frag_avg_s / 1e9
-    workload = f'{a.scene}/{a.pose}/{W}x{H}/N{N}'
+    workload = f'{a.scene}/{a.pose}/{W}x{H}/N{len(devices)}'
 
-    result = None
-    if rank == 0:
-        e2e = None
-        if not a.no_e2e and N == 1:
-            # updateAndRender into a caller-owned host buffer: includes the D2H over PCIe
-            host = np.empty((H, W), dtype=np.uint32)
-            r.configure(data_path, local)
-            for t in script:
-                r.update_and_render(W, H, t, host)
-            for _ in range(5):
-                r.update_and_render(W, H, hold, host)
-            n_e2e = max(20, min(200, a.steps))
-            t1 = time.perf_counter()
-            for _ in range(n_e2e):
-                r.update_and_render(W, H, hold, host)
-            e2e = n_e2e / (time.perf_counter() - t1)
-        cpu = None
-        if not a.no_cpu_baseline and N == 1:
-            cfps, cframes, cel = cpu_baseline(data_path, script, hold, W, H, a.cpu_seconds)
-            cpu = {'value': round(cfps, 4), 'unit': 'frames/s', 'cores': 1, 'kind': 'port',
-                   'sample': f'{cframes} frames of {a.scene}/{a.pose} at {W}x{H} in {cel:.1f} s, single thread, '
-                             f'oracle/render_oracle.c (gcc -O2) on {cpu_model()}'}
-        result = {
-            'metric': METRIC,
-            'value': round(fps, 3),
-            'unit': 'frames/s',
-            'n_gpus': N,
-            'steps': a.steps,
-            'warmup': a.warmup,
-            'ms_per_step': round(el / a.steps * 1e3, 5),
-            'higher_is_better': True,
-            'scaling': 'strong',
-            'vs_baseline': None,
-            'dtype': 'f32',
-            'data': 'synthetic: deterministic data.bin-format scene (SplitMix64 geometry, procedural ripmaps)',
-            'config': {'workload': f'updateAndRender frame, scene {a.scene} ({nslots // 2} triangles, '
-                                   f'{ntex >> 18} ripmap textures), pose {a.pose}, {W}x{H}',
-                       'fragment_path': {1: 'rows', 2: 'tiles'}.get(path, '?'),
-                       'scene': a.scene, 'pose': a.pose, 'width': W, 'height': H,
-                       'band_rows': B if N > 1 else H, 'parallelism': f'rows{N}' + (' (interleaved bands; gather timed separately)' if N > 1 else '')},
-            'mpixels_per_s': round(fps * W * H / 1e6, 2),
-            'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
-            'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
-            # N = 1: updateAndRender into a host buffer; N > 1: every rank's bands into one shared host frame
-            'e2e_fps_with_d2h': round(e2e, 3) if e2e else (round(e2e_multi, 3) if e2e_multi else None),
-            'gathered_fps': round(gathered_fps, 3) if gathered_fps else None,
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
-                         'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes},
-            'cpu_baseline': cpu,
-        }
-        print(json.dumps(result), flush=True)
+    # device-resident rate of one GPU: whole frames pipelined into HBM (no host copy)
+    device_fps = None
+    if not a.no_device:
+        r.configure_devices([], B)
+        r.configure(data_path, devices[0])
+        out = torch.empty((H, W), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        for t in script:
+            r.render_bands(t, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
+        for _ in range(warmup):
+            r.render_bands(hold_in, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r.render_bands(hold_in, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        device_fps = steps / (time.perf_counter() - t0)
+        del out
+
+    cpu = None
+    if not a.no_cpu_baseline and len(devices) == 1:
+        cfps, cframes, cel = cpu_baseline(data_path, script, hold, W, H, a.cpu_seconds)
+        cpu = {'value': round(cfps, 4), 'unit': 'frames/s', 'cores': 1, 'kind': 'port',
+               'sample': f'{cframes} frames of {a.scene}/{a.pose} at {W}x{H} in {cel:.1f} s, single thread, '
+                         f'oracle/render_oracle.c (gcc -O2) on {cpu_model()}'}
     r.shutdown()
-    if N > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return result
+    buf.free()
+
+    frame_bytes = 4 * W * H
+    return {
+        'metric': METRIC,
+        'value': round(fps, 3),
+        'unit': 'frames/s',
+        'n_gpus': N,
+        'steps': steps,
+        'warmup': warmup,
+        'ms_per_step': round(total / steps * 1e3, 5),
+        'higher_is_better': True,
+        'scaling': 'strong',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic: deterministic data.bin-format scene (SplitMix64 geometry, procedural ripmaps)',
+        'config': {'workload': f'updateAndRender into the caller\'s host double buffer, scene {a.scene} '
+                               f'({nslots // 2} triangles, {ntex >> 18} ripmap textures), pose {a.pose}, {W}x{H}',
+                   'fragment_path': {1: 'rows', 2: 'tiles'}.get(path, '?'),
+                   'scene': a.scene, 'pose': a.pose, 'width': W, 'height': H, 'devices': devices,
+                   'band_rows': B if len(devices) > 1 else H,
+                   'parallelism': f'rows{len(devices)}' + (' (interleaved bands, per-device D2H into the caller buffer, '
+                                                           'one process)' if len(devices) > 1 else '')},
+        'mpixels_per_s': round(fps * W * H / 1e6, 2),
+        'median_ms': round(median_s * 1e3, 5),
+        'p10_ms': round(float(np.percentile(per, 10)) * 1e3, 5),
+        'p90_ms': round(float(np.percentile(per, 90)) * 1e3, 5),
+        'fps_mean': round(steps / total, 3),
+        'delivery_GB_per_s': round(frame_bytes / median_s / 1e9, 3),
+        'host_buffer': {'halves_pinned': halves_pinned, 'pinned_frames': host['pinned_frames'],
+                        'pageable_frames': host['pageable_frames']},
+        'device_fps': round(device_fps, 3) if device_fps else None,
+        'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
+        'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
+                     'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,
+                     'launch': f'device 0 part ({rows0} of {H} rows) during the updateAndRender frames'},
+        'cpu_baseline': cpu,
+    }
 
 
 if __name__ == '__main__':

@@ -51,6 +51,22 @@ void updateAndRender(const PixelData *pixel_data, const Input *input);
  * Environment overrides: S3R_DATA_PATH, S3R_DEVICE.  Returns 0. */
 int s3r_configure(const char *data_path, int device);
 
+/* Several GPUs behind updateAndRender (the reference's one call per frame, main.swift:121 ->
+ * render.cpp:264-265, from one thread).  With n_devices > 1, every updateAndRender splits the
+ * frame's rows into interleaved bands of band_rows rows (0: S3R_BAND or 16) -- frame row y belongs to
+ * device ((y / band_rows) % n_devices) -- and each device renders its bands and copies them
+ * straight into their rows of pixel_data->buffer over its own PCIe link, device 0 on the calling
+ * thread and the others on one library worker thread each; the call returns when every part has
+ * landed.  Pixels are identical to the one-device frame.  n_devices = 0 restores one device
+ * (s3r_configure's).  The same ids may repeat (parts on one GPU: tests).  For a caller that only
+ * binds updateAndRender (the Swift app), S3R_DEVICES="0,1,2,..." selects the devices instead.  Drops
+ * all state like s3r_configure.  Returns 0, or -1 on bad arguments (negative id, n_devices > 64). */
+int s3r_configure_devices(const int *device_ids, int n_devices, uint32_t band_rows);
+
+/* The devices updateAndRender uses (after init: the ones in use); writes up to max_ids ids and
+ * returns the count. */
+int s3r_devices(int *out_ids, int max_ids);
+
 /* Release every GPU resource and registered host buffer; the next call re-initialises. */
 void s3r_shutdown(void);
 
@@ -92,6 +108,17 @@ int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t hei
  * a no-op for a pointer the library never registered.  For host frames about to be unmapped or freed
  * (updateAndRender buffers need not: a stale registration is detected and replaced there). */
 void s3r_unregister_host(void *ptr);
+
+/* Host buffers.  updateAndRender page-locks the caller's buffer (hipHostRegister, cached) so the
+ * frame's copy runs at the pinned DMA rate.  Registrations are whole pages; a buffer overlapping an
+ * existing registration -- the second half of the reference's double buffer (one 2 * bufferSize
+ * allocation, main.swift:164) shares the seam page with the first -- is merged with it into one
+ * registration covering both.  s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful
+ * registration.  s3r_host_stats: {frames copied into a pinned buffer, frames copied into a pageable
+ * one, successful registrations, registrations merged into a larger one, registrations held, stale
+ * registrations replaced}. */
+int s3r_host_pinned(const void *ptr, uint64_t bytes);
+void s3r_host_stats(uint64_t out[6]);
 
 /* Rows of a height-row frame owned by `part`. */
 uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);

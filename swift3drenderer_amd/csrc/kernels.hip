@@ -342,6 +342,10 @@ struct FragShared {
     uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
 };
 static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
+// k_fragment stages a bin's pair records in tab4 before the chunk loop (s3r_kernels.h kPairMax x
+// kPairWords uint4): a tuning build with fewer tables must still leave room for them.
+static_assert(sizeof(((FragShared *)nullptr)->tab4) >= 64u * 8u * sizeof(uint4),
+              "pair staging (kPairMax * kPairWords uint4) must fit in tab4");
 constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask, uint32_t lane) {
@@ -952,7 +956,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t segs,
                                                   uint32_t rows_local,
                                                   uint32_t *__restrict__ bincnt,
-                                                  const uint4 *__restrict__ pairs, uint32_t done_tag, uint32_t *done_flag,
+                                                  const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order) {
     __shared__ FragShared sh;
     S3R_WGT(0);
@@ -1986,6 +1990,10 @@ void stats_read(unsigned long long out[24], bool reset) {
 constexpr uint32_t kSegChunks = S3R_SEG_PIXELS / kChunk;   // widest fragment segment, in chunks
 static_assert(kSegChunks * kChunk == S3R_SEG_PIXELS, "segment = whole chunks");
 static_assert(kSegChunks == 6, "k_fragment instantiations below: 6, 3, 2, 1 chunks");
+// k_geometry's to_pairs maps start-table points (multiples of kStartPx) to the segments they start:
+// every segment width the build can choose must divide kStartPx.
+static_assert(kStartPx % (kChunk * 6u) == 0 && kStartPx % (kChunk * 3u) == 0 && kStartPx % (kChunk * 2u) == 0 &&
+              kStartPx % kChunk == 0, "fragment segment widths must divide the start-table spacing");
 
 // Segment width of this frame's row path: the widest of 6, 3, 2, 1 chunks that still launches at
 // least kMinFragBlocks workgroups (~8 per CU), so small frames fill the chip (a 1080p frame at
@@ -1994,7 +2002,9 @@ static_assert(kSegChunks == 6, "k_fragment instantiations below: 6, 3, 2, 1 chun
 // 3-chunk segments were chosen (1080p: 2 700 workgroups; 1/4 of 4K: 2 700) 2-chunk ones (4 050) were
 // faster (1080p flat 31.6k -> 34.3k fps, 4K part 1/4 38.7k -> 40.8k); elsewhere the choice is unchanged.
 constexpr uint64_t kMinFragBlocks = 2000;   // measured best or near-best for 4K at 1, 2, 4, 8 row-band parts and 1080p
-static uint32_t g_segch = kSegChunks;
+// per host thread: with several devices behind updateAndRender each device's worker thread configures
+// and launches its own frame part (render_api.cpp), and parts may differ in rows
+static thread_local uint32_t g_segch = kSegChunks;
 
 void fragment_configure(uint32_t W, uint32_t rows_local) {
     const char *mb_env = getenv("S3R_MIN_BLOCKS");                                  // tuning / test override
@@ -2036,7 +2046,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs, uint32_t tag,
+                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
@@ -2050,11 +2060,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
               : g_segch == 3 ? k_fragment<3, false> : g_segch == 2 ? k_fragment<2, false> : k_fragment<1, false>;
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
-                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs, tag,
+                              rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
                               done_flag, prev_tag, order);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
-                           W, H, band, nparts, part, segs, rows_local, bincnt, pairs, tag, done_flag, prev_tag, order);
+                           W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

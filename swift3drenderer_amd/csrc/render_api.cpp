@@ -7,15 +7,30 @@
 //
 // State is process-global like the reference's statics (render.cpp:51-113); calls are expected from
 // one thread at a time (main.swift calls from its main-thread timer only).
+//
+// Devices.  The camera, the scene's counts and the caller's host-buffer registrations are the
+// library's (Lib); everything that lives on a GPU -- the scene replica, the per-frame buffer sets,
+// streams and frame tags -- is one Dev per device.  With one device (the default) updateAndRender
+// renders the whole frame on it.  With N devices (s3r_configure_devices, or S3R_DEVICES=0,1,... for a
+// caller that only knows updateAndRender, like the Swift app) the frame's rows are split into
+// interleaved bands (band b -> device b % N) and every device renders its bands and
+// copies them straight into their rows of the caller's buffer over its own PCIe link; device 0's
+// part runs on the calling thread, the others on one persistent worker thread per device, so the
+// devices' HIP calls do not serialise.  The call returns when every part has landed.
 #include <dlfcn.h>
 #include <limits.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/render.h"
@@ -46,28 +61,38 @@ constexpr int kSets = 4;
 #endif
 constexpr int kGeoStreams = S3R_GEO_STREAMS;
 constexpr uint64_t kLptMinBins = 4000;      // longest-first fragment order from this many bins (~3 rounds; see render_core)
+constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
+constexpr int kMaxDevices = 64;
 
-struct Lib {
-    bool initialized = false;
-    std::string data_path;     // "" = reference search
+// S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
+struct HostProf {
+    bool on = getenv("S3R_HOSTPROF") != nullptr;
+    double t[6] = {};
+    uint64_t frames = 0;
+    std::chrono::steady_clock::time_point last;
+    void start() { if (on) last = std::chrono::steady_clock::now(); }
+    void lap(int i) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        t[i] += std::chrono::duration<double, std::micro>(now - last).count();
+        last = now;
+    }
+    void report(int device) {
+        if (!on || !frames) return;
+        fprintf(stderr, "s3r hostprof device %d (us/frame over %llu): begin %.2f  prep %.2f  geo-wait %.2f  "
+                "geo-launch %.2f  frag-wait %.2f  frag-launch %.2f\n", device, (unsigned long long)frames,
+                t[0] / frames, t[1] / frames, t[2] / frames, t[3] / frames, t[4] / frames, t[5] / frames);
+    }
+};
+
+// One GPU: its replica of the scene, its per-frame buffer sets, streams and frame tags.
+struct Dev {
     int device = -1;
-
-    // camera state, render.cpp:51-65
-    F3 pos{0, 0, 0}, ax{1, 0, 0}, ay{0, 1, 0}, az{0, 0, 1};
-    Mat34 m{{{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}}};
-    float mouse[2] = {0, 0};
-    // config, render.cpp:81-97
-    float factor = 1;
-    uint32_t depth_buffer_size = 0;
-
-    // scene on the device
-    uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
-    uint64_t nindices = 0;
     float4 *vtx = nullptr, *nrm = nullptr, *pay = nullptr;
     uint8_t *disc = nullptr;
     uint32_t *vidx = nullptr, *aidx = nullptr, *tex = nullptr;
-    // per-frame geometry, double-buffered: frame k's geometry (k_geometry on stream `geo`) overlaps
-    // frame k-1's fragment kernel on the caller's stream
+    // per-frame geometry, kSets buffer sets: frame k's geometry (k_geometry on a geometry stream)
+    // overlaps earlier frames' fragment kernels on the caller's stream
     TriSetup *tris[kSets] = {};
     float *rowtab[kSets] = {};     // 2T x rows x (segments + 1) x float4 exact row starts
     size_t rowtab_cap = 0;
@@ -88,16 +113,14 @@ struct Lib {
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
     uint32_t *tile_total_host = nullptr;       // pinned: (total, appended) per buffer set
-    int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
-    bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
     // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
-    // fragment launch (complete by stream order) in *done_host (host-coherent memory;
-    // done_dev is its device address); issued_tag[p] = the tag of the last fragment launch that read
-    // set p (0: none); last_tag = the previous row-path fragment launch, last_stream = the stream of
-    // the previous frame (either path)
+    // fragment launch (complete by stream order) in *done_host (host-coherent memory; done_dev is its
+    // device address); issued_tag[p] = the tag of the last fragment launch that read set p (0: none);
+    // last_tag = the previous row-path fragment launch, last_stream = the stream of the previous frame
+    // (either path)
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
@@ -107,42 +130,149 @@ struct Lib {
     bool have_last = false;
     hipEvent_t handoff = nullptr;
     uint32_t frame_no = 0;                     // frames issued: set frame_no % kSets
-    uint32_t *frame = nullptr;
+    uint32_t *frame = nullptr;                 // updateAndRender: this device's rows of the frame
     size_t frame_cap = 0;
     hipStream_t stream = nullptr, geo[kGeoStreams] = {};
-
-    // caller buffers registered as pinned memory (double buffer: main.swift:117-118)
-    struct Reg { void *p; size_t n; bool ok; };
-    std::vector<Reg> regs;
-    uint64_t stale_pins = 0;                   // registrations found stale and replaced (updateAndRender)
-
-    bool timing = false;
     std::vector<TimingSlot> tslots;
     size_t tcount = 0;
+    HostProf hp;
+};
+
+// The scene as read from data.bin (render.cpp:177-209), converted to the device layout once and
+// uploaded to every device.
+struct HostScene {
+    std::vector<float4> vtx, nrm, pay;
+    std::vector<uint8_t> disc;
+    std::vector<uint32_t> vidx, aidx, tex;
+};
+
+// Persistent worker threads, one per device beyond the first: run(fn, arg, n) calls fn(arg, 0) on
+// the calling thread and fn(arg, i) on worker i for 0 < i < n, and returns when all have returned.
+// Workers spin briefly on the frame generation (back-to-back frames hand over in ~1 us) and then
+// sleep on a condition variable (a 60 Hz caller does not keep cores busy).
+class Pool {
+  public:
+    void start(int workers) {
+        stop();
+        stop_.store(false);
+        // each worker starts from the generation of now: a run() issued before it is scheduled is
+        // still seen as new
+        const uint64_t g0 = gen_.load(std::memory_order_acquire);
+        for (int i = 1; i <= workers; i++) th_.emplace_back([this, i, g0] { loop(i, g0); });
+    }
+    void stop() {
+        if (th_.empty()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_.store(true);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_work_.notify_all();
+        for (auto &t : th_) t.join();
+        th_.clear();
+    }
+    void run(void (*fn)(void *, int), void *arg, int n) {
+        if (n > 1) {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                fn_ = fn;
+                arg_ = arg;
+                active_ = n;
+                pending_.store(n - 1, std::memory_order_relaxed);
+                gen_.fetch_add(1, std::memory_order_release);
+            }
+            cv_work_.notify_all();
+        }
+        fn(arg, 0);
+        if (n > 1) {
+            if (!spin([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
+            }
+        }
+    }
+    ~Pool() { stop(); }
+
+  private:
+    template <class Pred> static bool spin(Pred done) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 1;; k++) {
+            if (done()) return true;
+            __builtin_ia32_pause();
+            if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) return done();
+        }
+    }
+    void loop(int idx, uint64_t seen) {
+        for (;;) {
+            if (!spin([&] { return gen_.load(std::memory_order_acquire) != seen; })) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_work_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+            }
+            seen = gen_.load(std::memory_order_acquire);
+            if (stop_.load()) return;
+            void (*fn)(void *, int);
+            void *arg;
+            int active;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                fn = fn_; arg = arg_; active = active_;
+            }
+            if (idx >= active) continue;     // (run() with fewer parts than workers: not used)
+            fn(arg, idx);
+            if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                cv_done_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_work_, cv_done_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<bool> stop_{false};
+    void (*fn_)(void *, int) = nullptr;
+    void *arg_ = nullptr;
+    int active_ = 0;
+};
+
+struct Lib {
+    bool initialized = false;
+    std::string data_path;     // "" = reference search
+    int device = -1;           // s3r_configure: the single device (-1: S3R_DEVICE or the current one)
+    std::vector<int> device_ids;   // s3r_configure_devices: updateAndRender's devices (empty: single)
+    uint32_t band_rows = 0;        // rows per interleaved band across devices (0: S3R_BAND or 16)
+
+    // camera state, render.cpp:51-65
+    F3 pos{0, 0, 0}, ax{1, 0, 0}, ay{0, 1, 0}, az{0, 0, 1};
+    Mat34 m{{{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}}};
+    float mouse[2] = {0, 0};
+    // config, render.cpp:81-97
+    float factor = 1;
+    uint32_t depth_buffer_size = 0;
+
+    // scene counts (the same on every device)
+    uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
+    uint64_t nindices = 0;
+    int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
+    bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
+    bool timing = false;
+
+    std::vector<Dev *> devs;                   // devs[0]: s3r_render_bands' device, updateAndRender's first
+    uint32_t band = kDefaultBand;              // resolved band_rows
+    Pool pool;
+
+    // caller buffers registered as pinned memory (the double buffer: main.swift:117-118, :164):
+    // page-aligned, disjoint ranges [a, b); a request overlapping existing ranges is merged with them
+    // into one registration, so two halves of one allocation -- which share the page at the seam --
+    // end up in one registration that covers both
+    struct Reg { uintptr_t a, b; bool ok; };
+    std::vector<Reg> regs;
+    uint64_t stale_pins = 0;                   // registrations found stale and replaced (updateAndRender)
+    uint64_t pinned_frames = 0, pageable_frames = 0, registrations = 0, merges = 0;
 };
 
 Lib g;
-
-// S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
-struct HostProf {
-    bool on = getenv("S3R_HOSTPROF") != nullptr;
-    double t[6] = {};
-    uint64_t frames = 0;
-    std::chrono::steady_clock::time_point last;
-    void start() { if (on) last = std::chrono::steady_clock::now(); }
-    void lap(int i) {
-        if (!on) return;
-        const auto now = std::chrono::steady_clock::now();
-        t[i] += std::chrono::duration<double, std::micro>(now - last).count();
-        last = now;
-    }
-    void report() {
-        if (!on || !frames) return;
-        fprintf(stderr, "s3r hostprof (us/frame over %llu): begin %.2f  prep %.2f  geo-wait %.2f  geo-launch %.2f  "
-                "frag-wait %.2f  frag-launch %.2f\n", (unsigned long long)frames, t[0] / frames, t[1] / frames,
-                t[2] / frames, t[3] / frames, t[4] / frames, t[5] / frames);
-    }
-} hp;
 
 float config_scale() {
     const float fov = (float)M_PI / 5.f;        // render.cpp:91
@@ -217,7 +347,7 @@ template <class T> T *dalloc(size_t n) {
     exit(666);
 }
 
-void initialize() {
+HostScene read_scene() {
     const std::string path = find_data_path();
     FILE *fp = path.empty() ? nullptr : fopen(path.c_str(), "rb");
     if (!fp) exit(666);                                                 // render.cpp:173
@@ -227,8 +357,9 @@ void initialize() {
     uint64_t cnt[2];
     rd(cnt, 16);
     const uint64_t nv = cnt[0];
-    std::vector<float4> vtx(nv);
-    rd(vtx.data(), nv * 16);
+    HostScene s;
+    s.vtx.resize(nv);
+    rd(s.vtx.data(), nv * 16);
     rd(cnt, 16);
     const uint64_t ni = cnt[0];
     std::vector<int64_t> vi(ni + ni % 2);
@@ -243,116 +374,189 @@ void initialize() {
     rd(ai.data(), ai.size() * 8);
     rd(cnt, 16);
     const uint64_t nt = cnt[0];
-    std::vector<uint32_t> tex(nt);
-    rd(tex.data(), nt * 4);
+    s.tex.resize(nt);
+    rd(s.tex.data(), nt * 4);
     fclose(fp);
 
     // The reference trusts the file; the GPU must not read out of bounds, so check it here.
     if (nv >= (1ull << 32) || na >= (1ull << 32) || nt >= (1ull << 32)) bad_scene(path, "too large");
     if (nai < ni) bad_scene(path, "fewer attribute indices than vertex indices");
     const uint64_t ntri = ni / 3;
-    std::vector<uint32_t> vi32(3 * ntri), ai32(3 * ntri);
+    s.vidx.resize(3 * ntri);
+    s.aidx.resize(3 * ntri);
     for (uint64_t k = 0; k < 3 * ntri; k++) {
         if (vi[k] < 0 || (uint64_t)vi[k] >= nv) bad_scene(path, "vertex index out of range");
         if (ai[k] < 0 || (uint64_t)ai[k] >= na) bad_scene(path, "attribute index out of range");
-        vi32[k] = (uint32_t)vi[k];
-        ai32[k] = (uint32_t)ai[k];
+        s.vidx[k] = (uint32_t)vi[k];
+        s.aidx[k] = (uint32_t)ai[k];
     }
-    std::vector<float4> nrm(na), pay(na);
-    std::vector<uint8_t> disc(na);
+    s.nrm.resize(na);
+    s.pay.resize(na);
+    s.disc.resize(na);
     for (uint64_t k = 0; k < na; k++) {
-        memcpy(&nrm[k], &attr[48 * k], 16);
-        memcpy(&pay[k], &attr[48 * k + 16], 16);
+        memcpy(&s.nrm[k], &attr[48 * k], 16);
+        memcpy(&s.pay[k], &attr[48 * k + 16], 16);
         uint32_t d;
         memcpy(&d, &attr[48 * k + 32], 4);                              // disc_t at +32
-        disc[k] = d != 0;
+        s.disc[k] = d != 0;
     }
-
-    if (g.device < 0) {
-        if (const char *e = getenv("S3R_DEVICE")) g.device = atoi(e);
-        else HIPCHECK(hipGetDevice(&g.device));
-    }
-    HIPCHECK(hipSetDevice(g.device));
-    if (!g.stream) HIPCHECK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-    g.serial = getenv("S3R_SERIAL") != nullptr;
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
-    g.vtx = dalloc<float4>(nv); g.nrm = dalloc<float4>(na); g.pay = dalloc<float4>(na);
-    g.disc = dalloc<uint8_t>(na);
-    g.vidx = dalloc<uint32_t>(3 * ntri); g.aidx = dalloc<uint32_t>(3 * ntri);
-    g.tex = dalloc<uint32_t>(nt);
+    return s;
+}
+
+void dev_init(Dev &d, const HostScene &s) {
+    HIPCHECK(hipSetDevice(d.device));
+    HIPCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    const uint32_t ntri = g.ntri;
+    d.vtx = dalloc<float4>(g.nv); d.nrm = dalloc<float4>(g.na); d.pay = dalloc<float4>(g.na);
+    d.disc = dalloc<uint8_t>(g.na);
+    d.vidx = dalloc<uint32_t>(3 * (size_t)ntri); d.aidx = dalloc<uint32_t>(3 * (size_t)ntri);
+    d.tex = dalloc<uint32_t>(g.ntex);
     for (int p = 0; p < kSets; p++) {
-        g.tris[p] = dalloc<TriSetup>(2 * ntri);
-        HIPCHECK(hipEventCreateWithFlags(&g.geo_done[p], hipEventDisableTiming));
-        HIPCHECK(hipEventCreateWithFlags(&g.frag_done[p], hipEventDisableTiming));
+        d.tris[p] = dalloc<TriSetup>(2 * (size_t)ntri);
+        HIPCHECK(hipEventCreateWithFlags(&d.geo_done[p], hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&d.frag_done[p], hipEventDisableTiming));
     }
     {
         void *h = nullptr;
         HIPCHECK(hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
         memset(h, 0, sizeof(uint32_t));
-        g.done_host = static_cast<volatile uint32_t *>(h);
-        HIPCHECK(hipHostGetDevicePointer((void **)&g.done_dev, h, 0));
-        HIPCHECK(hipEventCreateWithFlags(&g.handoff, hipEventDisableTiming));
+        d.done_host = static_cast<volatile uint32_t *>(h);
+        HIPCHECK(hipHostGetDevicePointer((void **)&d.done_dev, h, 0));
+        HIPCHECK(hipEventCreateWithFlags(&d.handoff, hipEventDisableTiming));
     }
     // geometry streams at the highest priority: their (small, latency-bound) workgroups are
     // dispatched as soon as the previous frame's fragment workgroups free a slot
     int prio_least = 0, prio_greatest = 0;
     HIPCHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-    for (hipStream_t &gs : g.geo)
-        if (!gs) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
-    HIPCHECK(hipMemcpy(g.vtx, vtx.data(), nv * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.nrm, nrm.data(), na * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.pay, pay.data(), na * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.disc, disc.data(), na, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.vidx, vi32.data(), 12 * ntri, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.aidx, ai32.data(), 12 * ntri, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(g.tex, tex.data(), nt * 4, hipMemcpyHostToDevice));
+    for (hipStream_t &gs : d.geo) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
+    HIPCHECK(hipMemcpy(d.vtx, s.vtx.data(), (size_t)g.nv * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.nrm, s.nrm.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.pay, s.pay.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.disc, s.disc.data(), g.na, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.vidx, s.vidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.aidx, s.aidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d.tex, s.tex.data(), (size_t)g.ntex * 4, hipMemcpyHostToDevice));
 }
 
+// "0,1,2" -> {0, 1, 2}; empty on a malformed list.
+std::vector<int> parse_devices(const char *s) {
+    std::vector<int> ids;
+    while (s && *s) {
+        char *end = nullptr;
+        const long v = strtol(s, &end, 10);
+        if (end == s || v < 0 || v > INT_MAX) return {};
+        ids.push_back((int)v);
+        s = end;
+        while (*s == ',' || *s == ' ') s++;
+    }
+    if ((int)ids.size() > kMaxDevices) return {};
+    return ids;
+}
+
+void initialize() {
+    const HostScene s = read_scene();
+    std::vector<int> ids = g.device_ids;
+    if (ids.empty()) ids = parse_devices(getenv("S3R_DEVICES"));
+    if (ids.empty()) {
+        int dev = g.device;
+        if (dev < 0) {
+            if (const char *e = getenv("S3R_DEVICE")) dev = atoi(e);
+            else HIPCHECK(hipGetDevice(&dev));
+        }
+        ids.push_back(dev);
+    }
+    g.band = g.band_rows;
+    if (!g.band) {
+        const char *e = getenv("S3R_BAND");
+        g.band = e && atoi(e) > 0 ? (uint32_t)atoi(e) : kDefaultBand;
+    }
+    g.serial = getenv("S3R_SERIAL") != nullptr;
+    for (int id : ids) {
+        Dev *d = new Dev();
+        d->device = id;
+        dev_init(*d, s);
+        g.devs.push_back(d);
+    }
+    HIPCHECK(hipSetDevice(g.devs[0]->device));
+    if (g.devs.size() > 1) g.pool.start((int)g.devs.size() - 1);
+}
+
+// Wait for every device of the library (no copy into a caller buffer may still be in flight).
+void drain_devices() {
+    for (Dev *d : g.devs) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipDeviceSynchronize());
+    }
+    if (g.devs.empty()) HIPCHECK(hipDeviceSynchronize());
+    else HIPCHECK(hipSetDevice(g.devs[0]->device));
+}
+
+// Drops every host registration.  A registration may belong to a host frame s3r_bands_to_host is
+// still filling (its copies are asynchronous), so the devices are drained first.
 void unregister_all() {
+    bool any = false;
+    for (auto &r : g.regs) any |= r.ok;
+    if (any) drain_devices();
     for (auto &r : g.regs)
-        if (r.ok) (void)hipHostUnregister(r.p);
+        if (r.ok) (void)hipHostUnregister((void *)r.a);
     g.regs.clear();
 }
 
-void release_all() {
-    if (g.initialized) {
-        (void)hipSetDevice(g.device);
-        if (g.stream) (void)hipStreamSynchronize(g.stream);
-        for (hipStream_t gs : g.geo)
-            if (gs) (void)hipStreamSynchronize(gs);
-        (void)hipDeviceSynchronize();
-        unregister_all();
-        void *ptrs[] = {g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.tex, g.frame, g.keys};
-        for (void *p : ptrs)
+void dev_release(Dev &d) {
+    (void)hipSetDevice(d.device);
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
+        void *set[] = {d.tris[q], d.rowtab[q], d.bincnt[q], d.pairs[q], d.order[q], d.tile_counts[q], d.tile_offs[q],
+                       d.tile_cursor[q], d.tile_list[q], d.recs[q], d.boxes[q], d.app_list[q], d.app_count[q]};
+        for (void *p : set)
             if (p) (void)hipFree(p);
-        for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
-            void *set[] = {g.tris[q], g.rowtab[q], g.bincnt[q], g.pairs[q], g.order[q], g.tile_counts[q], g.tile_offs[q], g.tile_cursor[q],
-                           g.tile_list[q], g.recs[q], g.boxes[q], g.app_list[q], g.app_count[q]};
-            for (void *p : set)
-                if (p) (void)hipFree(p);
+    }
+    if (d.done_host) (void)hipHostFree((void *)d.done_host);
+    if (d.handoff) (void)hipEventDestroy(d.handoff);
+    if (d.tile_total_host) (void)hipHostFree(d.tile_total_host);
+    for (int p = 0; p < kSets; p++) {
+        if (d.geo_done[p]) (void)hipEventDestroy(d.geo_done[p]);
+        if (d.frag_done[p]) (void)hipEventDestroy(d.frag_done[p]);
+    }
+    for (hipStream_t gs : d.geo)
+        if (gs) (void)hipStreamDestroy(gs);
+    for (auto &t : d.tslots) {
+        (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
+    }
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+}
+
+void release_all() {
+    g.pool.stop();
+    if (g.initialized) {
+        for (Dev *d : g.devs) {
+            (void)hipSetDevice(d->device);
+            (void)hipDeviceSynchronize();
         }
-        if (g.done_host) (void)hipHostFree((void *)g.done_host);
-        if (g.handoff) (void)hipEventDestroy(g.handoff);
-        if (g.tile_total_host) (void)hipHostFree(g.tile_total_host);
-        for (int p = 0; p < kSets; p++) {
-            if (g.geo_done[p]) (void)hipEventDestroy(g.geo_done[p]);
-            if (g.frag_done[p]) (void)hipEventDestroy(g.frag_done[p]);
+        unregister_all();
+        for (Dev *d : g.devs) {
+            dev_release(*d);
+            delete d;
         }
-        for (hipStream_t gs : g.geo)
-            if (gs) (void)hipStreamDestroy(gs);
-        for (auto &t : g.tslots) {
-            (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
-        }
-        if (g.stream) (void)hipStreamDestroy(g.stream);
+        g.devs.clear();
+    } else {
+        unregister_all();
     }
     const std::string path = g.data_path;
     const int dev = g.device, rp = g.raster_path;
+    const std::vector<int> ids = g.device_ids;
+    const uint32_t band = g.band_rows;
     g.~Lib();
     new (&g) Lib();
     g.data_path = path;
     g.device = dev;
     g.raster_path = rp;
+    g.device_ids = ids;
+    g.band_rows = band;
 }
 
 // render.cpp:266-280: first-call init, camera, resize.
@@ -363,7 +567,7 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
         update_camera(input, true);
     } else {
         update_camera(input, false);
-        HIPCHECK(hipSetDevice(g.device));
+        HIPCHECK(hipSetDevice(g.devs[0]->device));
     }
     const uint32_t dbs = width * height * (uint32_t)sizeof(float);
     if (g.depth_buffer_size != dbs) {
@@ -373,38 +577,40 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
     }
 }
 
-TimingSlot *timing_slot() {
+TimingSlot *timing_slot(Dev &d) {
     if (!g.timing) return nullptr;
-    if (g.tcount == g.tslots.size()) {
+    if (d.tcount == d.tslots.size()) {
         TimingSlot t;
         HIPCHECK(hipEventCreate(&t.frame0)); HIPCHECK(hipEventCreate(&t.frag0)); HIPCHECK(hipEventCreate(&t.frag1));
-        g.tslots.push_back(t);
+        d.tslots.push_back(t);
     }
-    return &g.tslots[g.tcount++];
+    return &d.tslots[d.tcount++];
 }
 
-// Frame tags are the uint32 frame number (0 = none): the slot-mask words' high halves, issued_tag,
-// last_tag and the completion word.  Before the count wraps (~62 h at 19 k fps) every stream is
-// drained, the slot masks are zeroed and the count restarts, so no tag is reused while a word or a
-// completion flag still carries it.
+// Frame tags are the uint32 frame number (0 = none): issued_tag, last_tag and the completion word
+// k_fragment's first workgroup stores.  Before the count wraps (~62 h at 19 k fps) every stream is
+// drained, the completion word and issued tags are reset and the count restarts, so no tag is
+// reused while the completion word may still carry it.  The bins' pair counts are reset by the
+// fragment workgroups that read them (the set's last reader); they are zeroed here as well, in case
+// a frame was abandoned between its geometry and fragment launches.
 constexpr uint32_t kTagLimit = 0xFFFFFF00u;
 
-void restart_tags(uint32_t next_frame_no) {
+void restart_tags(Dev &d, uint32_t next_frame_no) {
     HIPCHECK(hipDeviceSynchronize());
     for (int p = 0; p < kSets; p++)
-        if (g.bincnt[p]) HIPCHECK(hipMemset(g.bincnt[p], 0, g.bins_cap * sizeof(uint32_t)));
+        if (d.bincnt[p]) HIPCHECK(hipMemset(d.bincnt[p], 0, d.bins_cap * sizeof(uint32_t)));
     HIPCHECK(hipDeviceSynchronize());
-    g.frame_no = next_frame_no;
-    for (uint32_t &t : g.issued_tag) t = 0;
-    g.last_tag = 0;
-    if (g.done_host) __atomic_store_n(g.done_host, 0u, __ATOMIC_RELEASE);
+    d.frame_no = next_frame_no;
+    for (uint32_t &t : d.issued_tag) t = 0;
+    d.last_tag = 0;
+    if (d.done_host) __atomic_store_n(d.done_host, 0u, __ATOMIC_RELEASE);
 }
 
 // The buffer set of the frame being issued; frames cycle through kSets sets.
-uint32_t next_set() {
-    if (g.frame_no >= kTagLimit) restart_tags(0);
-    g.frame_no++;
-    return g.frame_no % kSets;
+uint32_t next_set(Dev &d) {
+    if (d.frame_no >= kTagLimit) restart_tags(d, 0);
+    d.frame_no++;
+    return d.frame_no % kSets;
 }
 
 // Row path: block until the last fragment kernel that read buffer set p has finished.  *done_host
@@ -412,21 +618,21 @@ uint32_t next_set() {
 // its predecessor's tag there, and tags grow by frame.  Usually the set is free (the host runs at
 // most kSets frames ahead of the GPU); otherwise the launch after it -- issued already, in order on
 // the same stream -- reports it when it starts.
-void wait_set_free(uint32_t p) {
-    const uint32_t want = g.issued_tag[p];
-    if (want == 0 || __atomic_load_n(g.done_host, __ATOMIC_ACQUIRE) >= want) return;
-    if (want == g.last_tag) {
+void wait_set_free(Dev &d, uint32_t p) {
+    const uint32_t want = d.issued_tag[p];
+    if (want == 0 || __atomic_load_n(d.done_host, __ATOMIC_ACQUIRE) >= want) return;
+    if (want == d.last_tag) {
         // no row-path fragment launch after it to report it (tile-path frames followed): drain its stream
-        HIPCHECK(hipStreamSynchronize(g.last_stream));
-        __atomic_store_n(g.done_host, want, __ATOMIC_RELEASE);
+        HIPCHECK(hipStreamSynchronize(d.last_stream));
+        __atomic_store_n(d.done_host, want, __ATOMIC_RELEASE);
         return;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(g.done_host, __ATOMIC_ACQUIRE) < want) {
+    while (__atomic_load_n(d.done_host, __ATOMIC_ACQUIRE) < want) {
         __builtin_ia32_pause();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
             HIPCHECK(hipDeviceSynchronize());      // (never expected) surfaces a device fault
-            __atomic_store_n(g.done_host, g.last_tag, __ATOMIC_RELEASE);
+            __atomic_store_n(d.done_host, d.last_tag, __ATOMIC_RELEASE);
         }
     }
 }
@@ -434,20 +640,20 @@ void wait_set_free(uint32_t p) {
 // Frames are ordered on the caller's stream.  When a frame arrives on another stream than the
 // previous one, that stream first waits for the previous frame's fragment stage (one event): the
 // row path's completion chain (wait_set_free) and the tile path's shared key buffer assume it.
-void follow_previous_frame(hipStream_t st) {
+void follow_previous_frame(Dev &d, hipStream_t st) {
     // the null stream does not order our non-blocking streams (nor they it): a switch from or to
     // NULL needs the event like any other
-    if (g.have_last && st != g.last_stream) {
-        HIPCHECK(hipEventRecord(g.handoff, g.last_stream));
-        HIPCHECK(hipStreamWaitEvent(st, g.handoff, 0));
+    if (d.have_last && st != d.last_stream) {
+        HIPCHECK(hipEventRecord(d.handoff, d.last_stream));
+        HIPCHECK(hipStreamWaitEvent(st, d.handoff, 0));
     }
-    g.last_stream = st;
-    g.have_last = true;
+    d.last_stream = st;
+    d.have_last = true;
 }
 
 // S3R_SERIAL (profiling): the geometry waits for every earlier fragment kernel -- no overlap.
-void wait_all_fragments(hipStream_t geo) {
-    for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[q], 0));
+void wait_all_fragments(Dev &d, hipStream_t geo) {
+    for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[q], 0));
 }
 
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
@@ -460,7 +666,7 @@ bool use_tile_path() {
     return 2ull * g.ntri > kRowPathMaxSlots;
 }
 
-void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                   uint32_t *out, hipStream_t st, TimingSlot *ts) {
     if (W > 65535 || H > 65535) {                       // packed 16-bit bboxes
         fprintf(stderr, "s3r: tile path supports frames up to 65535 x 65535\n");
@@ -468,177 +674,219 @@ void render_tiles(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32
     }
     const float sw = (float)W, sh = (float)H;
     const uint64_t nt = tile_count(W, rows_local);
-    if (g.tiles_cap < nt) {
+    if (d.tiles_cap < nt) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
-            for (uint32_t **q : {&g.tile_counts[p], &g.tile_offs[p], &g.tile_cursor[p]}) {
+            for (uint32_t **q : {&d.tile_counts[p], &d.tile_offs[p], &d.tile_cursor[p]}) {
                 if (*q) HIPCHECK(hipFree(*q));
                 *q = dalloc<uint32_t>(nt);
             }
         }
-        g.tiles_cap = nt;
+        d.tiles_cap = nt;
     }
     const size_t npx = (size_t)W * rows_local;
-    if (g.keys_cap < npx) {                    // per-pixel winners (fragment stage, caller's stream)
+    if (d.keys_cap < npx) {                    // per-pixel winners (fragment stage, caller's stream)
         HIPCHECK(hipDeviceSynchronize());
-        if (g.keys) HIPCHECK(hipFree(g.keys));
-        g.keys = dalloc<unsigned long long>(npx);
-        g.keys_cap = npx;
+        if (d.keys) HIPCHECK(hipFree(d.keys));
+        d.keys = dalloc<unsigned long long>(npx);
+        d.keys_cap = npx;
     }
-    if (!g.recs[0]) {
+    if (!d.recs[0]) {
         for (int p = 0; p < kSets; p++) {
-            g.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
-            g.boxes[p] = dalloc<uint32_t>((size_t)2 * g.ntri);
-            g.app_list[p] = dalloc<uint32_t>(g.ntri);
-            g.app_count[p] = dalloc<uint32_t>(2);          // [0] appended count, [1] tile-pair total
-            g.tile_total[p] = g.app_count[p] + 1;
+            d.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
+            d.boxes[p] = dalloc<uint32_t>((size_t)2 * g.ntri);
+            d.app_list[p] = dalloc<uint32_t>(g.ntri);
+            d.app_count[p] = dalloc<uint32_t>(2);          // [0] appended count, [1] tile-pair total
+            d.tile_total[p] = d.app_count[p] + 1;
         }
-        HIPCHECK(hipHostMalloc((void **)&g.tile_total_host, 2 * kSets * sizeof(uint32_t)));
+        HIPCHECK(hipHostMalloc((void **)&d.tile_total_host, 2 * kSets * sizeof(uint32_t)));
     }
-    const uint32_t p = next_set();
-    hipStream_t geo = g.geo[0];
-    HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
-    if (g.serial) wait_all_fragments(geo);
+    const uint32_t p = next_set(d);
+    hipStream_t geo = d.geo[0];
+    HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[p], 0));
+    if (g.serial) wait_all_fragments(d, geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
-    launch_tile_setup(g.vtx, g.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, g.recs[p],
-                      g.boxes[p], g.app_list[p], g.app_count[p], g.tile_counts[p], g.tile_offs[p], g.tile_cursor[p],
-                      g.tile_total[p], geo);
+    launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
+                      d.boxes[p], d.app_list[p], d.app_count[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
+                      d.tile_total[p], geo);
     // the list size is data-dependent: read it back (the tile path's one host sync per frame)
-    uint32_t *host = g.tile_total_host + 2 * p;
-    HIPCHECK(hipMemcpyAsync(host, g.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
+    uint32_t *host = d.tile_total_host + 2 * p;
+    HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
     HIPCHECK(hipStreamSynchronize(geo));
     const uint32_t napp = host[0];
     const uint64_t total = host[1];
-    g.last_pairs = total;
-    g.last_path = 2;
-    if (g.tile_list_cap[p] < total) {
+    d.last_pairs = total;
+    d.last_path = 2;
+    if (d.tile_list_cap[p] < total) {
         HIPCHECK(hipDeviceSynchronize());
-        if (g.tile_list[p]) HIPCHECK(hipFree(g.tile_list[p]));
+        if (d.tile_list[p]) HIPCHECK(hipFree(d.tile_list[p]));
         const uint64_t cap = total + total / 4 + 1024;
-        g.tile_list[p] = dalloc<uint32_t>(cap);
-        g.tile_list_cap[p] = cap;
+        d.tile_list[p] = dalloc<uint32_t>(cap);
+        d.tile_list_cap[p] = cap;
     }
-    launch_tile_fill(g.boxes[p], g.ntri, g.recs[p], g.app_list[p], napp, W, band, nparts, part, g.tile_cursor[p],
-                     g.tile_list[p], geo);
-    HIPCHECK(hipEventRecord(g.geo_done[p], geo));
-    follow_previous_frame(st);
-    HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
+    launch_tile_fill(d.boxes[p], g.ntri, d.recs[p], d.app_list[p], napp, W, band, nparts, part, d.tile_cursor[p],
+                     d.tile_list[p], geo);
+    HIPCHECK(hipEventRecord(d.geo_done[p], geo));
+    follow_previous_frame(d, st);
+    HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_tile_raster(g.recs[p], W, band, nparts, part, rows_local, g.tile_offs[p], g.tile_counts[p], g.tile_list[p],
-                       g.keys, st);
-    launch_tile_resolve(g.keys, g.recs[p], g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, sw, sh,
-                        g.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
+    launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p], d.tile_list[p],
+                       d.keys, st);
+    launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
-    HIPCHECK(hipEventRecord(g.frag_done[p], st));
+    HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());
 }
 
-void render_core(uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
+// One frame part on device d (its current device must be set): rows_local rows of an interleaved
+// band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.
+void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st) {
-    TimingSlot *ts = timing_slot();
+    TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
-        render_tiles(W, H, band, nparts, part, rows_local, out, st, ts);
+        render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts);
         return;
     }
-    g.last_path = 1;
+    d.last_path = 1;
     fragment_configure(W, rows_local);
     const size_t need = (size_t)2 * g.ntri * rows_local * start_entries(W) * 4;
-    if (g.rowtab_cap < need) {
+    if (d.rowtab_cap < need) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
-            if (g.rowtab[p]) HIPCHECK(hipFree(g.rowtab[p]));
-            g.rowtab[p] = dalloc<float>(need);
+            if (d.rowtab[p]) HIPCHECK(hipFree(d.rowtab[p]));
+            d.rowtab[p] = dalloc<float>(need);
         }
-        g.rowtab_cap = need;
+        d.rowtab_cap = need;
     }
     const uint64_t nbins = fragment_bins(W, rows_local);
-    if (g.bins_cap < nbins) {
+    if (d.bins_cap < nbins) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
-            if (g.bincnt[p]) HIPCHECK(hipFree(g.bincnt[p]));
-            if (g.pairs[p]) HIPCHECK(hipFree(g.pairs[p]));
-            g.bincnt[p] = dalloc<uint32_t>(nbins);
-            g.pairs[p] = dalloc<uint4>(nbins * kPairMax * kPairWords);
-            HIPCHECK(hipMemset(g.bincnt[p], 0, nbins * sizeof(uint32_t)));
+            if (d.bincnt[p]) HIPCHECK(hipFree(d.bincnt[p]));
+            if (d.pairs[p]) HIPCHECK(hipFree(d.pairs[p]));
+            d.bincnt[p] = dalloc<uint32_t>(nbins);
+            d.pairs[p] = dalloc<uint4>(nbins * kPairMax * kPairWords);
+            HIPCHECK(hipMemset(d.bincnt[p], 0, nbins * sizeof(uint32_t)));
         }
         // hipMemset runs on the null stream, which does not order the non-blocking geometry
         // streams: finish it before the next k_geometry counts pairs in these bins
         HIPCHECK(hipDeviceSynchronize());
-        g.bins_cap = nbins;
+        d.bins_cap = nbins;
     }
     // longest-first order only where a launch is several rounds of resident workgroups (~1 280 on
     // the chip): a frame part of one round gains nothing and would pay the order column's time
-    const uint64_t bins = fragment_bins(W, rows_local);
+    const uint64_t bins = nbins;
     const char *lpt_env = getenv("S3R_LPT_MIN");            // tuning / test override
     const bool lpt = g.ntri > 0 && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins);
-    if (lpt && g.order_cap < bins) {
+    if (lpt && d.order_cap < bins) {
         HIPCHECK(hipDeviceSynchronize());
         for (int q = 0; q < kSets; q++) {
-            if (g.order[q]) HIPCHECK(hipFree(g.order[q]));
-            g.order[q] = dalloc<uint32_t>(2 * bins);
-            HIPCHECK(hipMemset(g.order[q], 0, 2 * bins * sizeof(uint32_t)));
+            if (d.order[q]) HIPCHECK(hipFree(d.order[q]));
+            d.order[q] = dalloc<uint32_t>(2 * bins);
+            HIPCHECK(hipMemset(d.order[q], 0, 2 * bins * sizeof(uint32_t)));
         }
-        HIPCHECK(hipDeviceSynchronize());     // (as for the slot masks: before k_geometry writes perm)
-        g.order_cap = bins;
+        HIPCHECK(hipDeviceSynchronize());     // (as for the bin counts: before k_geometry writes perm)
+        d.order_cap = bins;
     }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
-    const uint32_t p = next_set();
-    hipStream_t geo = g.geo[g.frame_no % kGeoStreams];
-    hp.lap(1);
+    const uint32_t p = next_set(d);
+    hipStream_t geo = d.geo[d.frame_no % kGeoStreams];
+    d.hp.lap(1);
     // the set's last reader (frame k - kSets) has usually finished: then no cross-stream wait
     if (g.serial) {
-        HIPCHECK(hipStreamWaitEvent(geo, g.frag_done[p], 0));
-        wait_all_fragments(geo);
+        HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[p], 0));
+        wait_all_fragments(d, geo);
     } else {
-        wait_set_free(p);
+        wait_set_free(d, p);
     }
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
-    hp.lap(2);
-    const uint32_t tag = g.frame_no;              // >= 1: frame k's tag for its slot masks and completion
-    launch_geometry(g.vtx, g.nrm, g.pay, g.disc, g.vidx, g.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, g.tris[p], g.rowtab[p], g.bincnt[p], g.pairs[p], geo, g.geo_done[p],
-                    lpt ? g.order[p] : nullptr);
-    hp.lap(3);
+    d.hp.lap(2);
+    const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
+    launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
+                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, d.geo_done[p],
+                    lpt ? d.order[p] : nullptr);
+    d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
-    // only where S3R_SERIAL waits on it
-    follow_previous_frame(st);
-    HIPCHECK(hipStreamWaitEvent(st, g.geo_done[p], 0));
-    hp.lap(4);
+    // only where S3R_SERIAL waits on it.  The fragment workgroups reset their bins' pair counts: the
+    // launch is the set's last reader, and the set's next geometry waits for it (wait_set_free).
+    follow_previous_frame(d, st);
+    HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
+    d.hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_fragment(g.tris[p], 2 * g.ntri, g.rowtab[p], g.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
-                    g.bincnt[p], g.pairs[p], tag, st, g.serial ? g.frag_done[p] : nullptr, g.done_dev, g.last_tag,
-                    lpt ? g.order[p] : nullptr);
-    g.issued_tag[p] = tag;
-    g.last_tag = tag;
+    launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
+                    d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
+                    lpt ? d.order[p] : nullptr);
+    d.issued_tag[p] = tag;
+    d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipGetLastError());
-    hp.lap(5);
-    hp.frames++;
+    d.hp.lap(5);
+    d.hp.frames++;
 }
 
-bool host_pinned(void *p, size_t n) {
+// ---------------------------------------------------------------- caller host buffers
+size_t page_size() {
+    static const size_t p = (size_t)sysconf(_SC_PAGESIZE);
+    return p;
+}
+
+// The registration covering [p, p + n), if any (ok or failed).
+Lib::Reg *find_reg(const void *p, size_t n) {
+    const uintptr_t a = (uintptr_t)p, b = a + n;
     for (auto &r : g.regs)
-        if (r.p == p && r.n == n) return r.ok;
+        if (r.a <= a && b <= r.b) return &r;
+    return nullptr;
+}
+
+void unregister_range(Lib::Reg &r) {
+    if (r.ok) (void)hipHostUnregister((void *)r.a);
+}
+
+// Page-lock [p, p + n) for DMA (cached).  The request is widened to whole pages; registrations it
+// overlaps -- the other half of a double buffer shares the seam page -- are dropped (after draining
+// the devices) and re-registered as one range covering the union, so each half of the reference's
+// double buffer lies inside ONE registration and its copy runs at the pinned rate.
+bool host_pinned(void *p, size_t n) {
+    if (Lib::Reg *r = find_reg(p, n)) return r->ok;
     if (getenv("S3R_NO_PIN")) return false;
+    const size_t pg = page_size();
+    uintptr_t a = (uintptr_t)p & ~(uintptr_t)(pg - 1);
+    uintptr_t b = ((uintptr_t)p + n + pg - 1) & ~(uintptr_t)(pg - 1);
+    bool drained = false;
+    for (size_t i = g.regs.size(); i-- > 0;) {
+        Lib::Reg &r = g.regs[i];
+        if (r.b <= a || b <= r.a) continue;
+        if (r.ok && !drained) { drain_devices(); drained = true; }
+        a = a < r.a ? a : r.a;
+        b = b > r.b ? b : r.b;
+        unregister_range(r);
+        g.regs.erase(g.regs.begin() + (long)i);
+        g.merges++;
+    }
     if (g.regs.size() >= 4) unregister_all();
-    const bool ok = hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
+    const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable) == hipSuccess;
     if (!ok) (void)hipGetLastError();
-    g.regs.push_back({p, n, ok});
+    else g.registrations++;
+    g.regs.push_back({a, b, ok});
     return ok;
 }
 
+// Drop the registration covering [p, p + n) (a stale one: its pages are no longer the caller's).
 void drop_registration(void *p, size_t n) {
     for (size_t i = 0; i < g.regs.size(); i++) {
-        if (g.regs[i].p == p && g.regs[i].n == n) {
-            if (g.regs[i].ok) (void)hipHostUnregister(p);
+        const uintptr_t a = (uintptr_t)p, b = a + n;
+        if (g.regs[i].a <= a && b <= g.regs[i].b) {
+            if (g.regs[i].ok) drain_devices();
+            unregister_range(g.regs[i]);
             g.regs.erase(g.regs.begin() + (long)i);
             return;
         }
     }
 }
 
-// A cached registration is keyed by (pointer, size).  If the caller freed its buffer and got a new
+// A cached registration is keyed by its address range.  If the caller freed its buffer and got a new
 // one at the same address, a registration that still pins the old pages would take the frame.
 // Pixels are 0x00RRGGBB, so a word with a set high byte is never a pixel: such a sentinel is stored
 // through the caller's pointer at the buffer's ends and every 64 KiB before the copy; if one
@@ -659,6 +907,69 @@ bool probes_overwritten(const uint32_t *buf, size_t words) {
     return b[words - 1] != kStaleProbe;
 }
 
+uint32_t band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part) {
+    if (band_rows == 0 || n_parts == 0 || part >= n_parts) return 0;
+    uint32_t rows = 0;
+    for (uint64_t b = part; b * band_rows < height; b += n_parts) {
+        const uint64_t y0 = b * band_rows;
+        rows += (uint32_t)((height - y0) < band_rows ? (height - y0) : band_rows);
+    }
+    return rows;
+}
+
+// One part's rows (compact on the device, as render_core wrote them) into their frame rows of a host
+// frame, asynchronously on st: one 2-D copy for the part's full bands (band_rows x W blocks spaced
+// n_parts bands apart) and one for a trailing partial band.
+void copy_bands_to_host(const uint32_t *dev_rows, uint32_t W, uint32_t H, uint32_t band_rows, uint32_t n_parts,
+                        uint32_t part, uint32_t *host_frame, hipStream_t st) {
+    const size_t rowb = (size_t)W * sizeof(uint32_t);
+    const uint32_t nbands = (H + band_rows - 1) / band_rows, last = nbands - 1u;
+    const uint32_t mine = (nbands > part) ? (nbands - part + n_parts - 1u) / n_parts : 0u;
+    const bool partial_last = (uint64_t)nbands * band_rows > H && last % n_parts == part;
+    const uint32_t full = mine - (partial_last ? 1u : 0u);
+    if (full)
+        HIPCHECK(hipMemcpy2DAsync(host_frame + (size_t)part * band_rows * W, (size_t)n_parts * band_rows * rowb, dev_rows,
+                                  (size_t)band_rows * rowb, (size_t)band_rows * rowb, full, hipMemcpyDeviceToHost, st));
+    if (partial_last)
+        HIPCHECK(hipMemcpyAsync(host_frame + (size_t)last * band_rows * W, dev_rows + (size_t)full * band_rows * W,
+                                (size_t)(H - last * band_rows) * rowb, hipMemcpyDeviceToHost, st));
+}
+
+// ---------------------------------------------------------------- updateAndRender's frame delivery
+struct Delivery {
+    uint32_t W, H, band, nparts;
+    uint32_t *host;            // the caller's buffer (whole frame)
+    size_t copy_bytes;         // single device: bytes of the frame copied (min(bufferSize, 4 W H))
+    bool copy_only;            // redo the copies of the frame already rendered (stale registration)
+};
+
+// Part i of the frame on device i: render its rows, copy them into the caller's buffer over this
+// device's link, wait for both.  Runs on the calling thread (i = 0) or device i's worker thread.
+void deliver_part(void *arg, int i) {
+    const Delivery &job = *static_cast<const Delivery *>(arg);
+    Dev &d = *g.devs[i];
+    HIPCHECK(hipSetDevice(d.device));
+    const uint32_t rows = job.nparts == 1 ? job.H : band_rows_local(job.H, job.band, job.nparts, (uint32_t)i);
+    if (rows && job.W) {
+        const size_t npx = (size_t)job.W * rows;
+        if (d.frame_cap < npx) {
+            if (d.frame) HIPCHECK(hipFree(d.frame));
+            d.frame = dalloc<uint32_t>(npx);
+            d.frame_cap = npx;
+        }
+        if (!job.copy_only)
+            render_core(d, job.W, job.H, job.nparts == 1 ? job.H : job.band, job.nparts, (uint32_t)i, rows, d.frame,
+                        d.stream);
+        if (job.nparts == 1) {
+            if (job.copy_bytes)
+                HIPCHECK(hipMemcpyAsync(job.host, d.frame, job.copy_bytes, hipMemcpyDeviceToHost, d.stream));
+        } else {
+            copy_bands_to_host(d.frame, job.W, job.H, job.band, job.nparts, (uint32_t)i, job.host, d.stream);
+        }
+    }
+    HIPCHECK(hipStreamSynchronize(d.stream));
+}
+
 }  // namespace
 
 extern "C" {
@@ -667,32 +978,32 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     const uint32_t W = pixel_data->width, H = pixel_data->height;
     frame_begin(input, W, H);
     const size_t npx = (size_t)W * H;
-    if (g.frame_cap < npx) {
-        if (g.frame) HIPCHECK(hipFree(g.frame));
-        g.frame = dalloc<uint32_t>(npx);
-        g.frame_cap = npx;
-    }
-    if (npx) render_core(W, H, H ? H : 1, 1, 0, H, g.frame, g.stream);
     // memset_pattern4 fills bufferSize bytes (render.cpp:282); the frame covers W*H pixels.
     const size_t frame_bytes = npx * 4;
     const size_t copy_bytes = pixel_data->bufferSize < frame_bytes ? pixel_data->bufferSize : frame_bytes;
     const size_t copy_words = copy_bytes / 4;
+    // several devices: each renders its interleaved bands and copies them into their rows (a caller
+    // buffer smaller than the frame -- not the reference's usage -- takes the one-device path)
+    const uint32_t ndev = (uint32_t)g.devs.size();
+    const uint32_t nparts = (ndev > 1 && copy_bytes == frame_bytes && H > g.band) ? ndev : 1u;
+    Delivery job{W, H, g.band, nparts, pixel_data->buffer, copy_bytes, false};
     bool pinned = false;
     if (copy_bytes) {
         pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
         if (pinned && copy_words) stamp_probes(pixel_data->buffer, copy_words);
-        HIPCHECK(hipMemcpyAsync(pixel_data->buffer, g.frame, copy_bytes, hipMemcpyDeviceToHost, g.stream));
+        (pinned ? g.pinned_frames : g.pageable_frames)++;
     }
+    if (npx) g.pool.run(deliver_part, &job, (int)nparts);
     for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
-    HIPCHECK(hipStreamSynchronize(g.stream));
     if (pinned && copy_words && !probes_overwritten(pixel_data->buffer, copy_words)) {
         // a stale registration (buffer freed and reallocated at the same address): pin anew, copy again
         drop_registration(pixel_data->buffer, pixel_data->bufferSize);
         g.stale_pins++;
         host_pinned(pixel_data->buffer, pixel_data->bufferSize);
-        HIPCHECK(hipMemcpyAsync(pixel_data->buffer, g.frame, copy_bytes, hipMemcpyDeviceToHost, g.stream));
-        HIPCHECK(hipStreamSynchronize(g.stream));
+        job.copy_only = true;
+        g.pool.run(deliver_part, &job, (int)nparts);
     }
+    HIPCHECK(hipSetDevice(g.devs[0]->device));
 }
 
 __attribute__((visibility("default"))) int s3r_configure(const char *data_path, int device) {
@@ -702,8 +1013,32 @@ __attribute__((visibility("default"))) int s3r_configure(const char *data_path, 
     return 0;
 }
 
+__attribute__((visibility("default"))) int s3r_configure_devices(const int *device_ids, int n_devices,
+                                                                uint32_t band_rows) {
+    if (n_devices < 0 || n_devices > kMaxDevices || (n_devices > 0 && !device_ids)) return -1;
+    for (int i = 0; i < n_devices; i++)
+        if (device_ids[i] < 0) return -1;
+    release_all();
+    g.device_ids.assign(device_ids, device_ids + n_devices);
+    g.band_rows = band_rows;
+    return 0;
+}
+
+__attribute__((visibility("default"))) int s3r_devices(int *out_ids, int max_ids) {
+    std::vector<int> ids;
+    if (g.initialized) {
+        for (Dev *d : g.devs) ids.push_back(d->device);
+    } else {
+        ids = g.device_ids;
+        if (ids.empty()) ids = parse_devices(getenv("S3R_DEVICES"));
+        if (ids.empty()) ids.push_back(g.device);
+    }
+    for (int i = 0; i < max_ids && i < (int)ids.size(); i++) out_ids[i] = ids[i];
+    return (int)ids.size();
+}
+
 __attribute__((visibility("default"))) void s3r_shutdown(void) {
-    hp.report();
+    for (Dev *d : g.devs) d->hp.report(d->device);
     release_all();
 }
 
@@ -717,99 +1052,114 @@ __attribute__((visibility("default"))) int s3r_raster_path(void) { return use_ti
 
 __attribute__((visibility("default"))) uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows,
                                                                    uint32_t n_parts, uint32_t part) {
-    if (band_rows == 0 || n_parts == 0 || part >= n_parts) return 0;
-    uint32_t rows = 0;
-    for (uint64_t b = part; b * band_rows < height; b += n_parts) {
-        const uint64_t y0 = b * band_rows;
-        rows += (uint32_t)((height - y0) < band_rows ? (height - y0) : band_rows);
-    }
-    return rows;
+    return band_rows_local(height, band_rows, n_parts, part);
 }
 
 __attribute__((visibility("default"))) int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height,
                                                                uint32_t band_rows, uint32_t n_parts, uint32_t part,
                                                                uint32_t *dev_out, void *stream) {
     if (band_rows == 0 || n_parts == 0 || part >= n_parts || (!dev_out && width && height)) return -1;
-    hp.start();
-    frame_begin(input, width, height);
-    hp.lap(0);
-    const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
-    // NULL is the legacy default (null) stream -- e.g. torch's default stream -- never our own.
-    hipStream_t st = (hipStream_t)stream;
-    if (rows && width) render_core(width, height, band_rows, n_parts, part, rows, dev_out, st);
+    hipStream_t st = (hipStream_t)stream;   // NULL is the legacy default (null) stream -- e.g. torch's default
+    if (!g.initialized) {
+        frame_begin(input, width, height);
+    } else {
+        g.devs[0]->hp.start();
+        frame_begin(input, width, height);
+        g.devs[0]->hp.lap(0);
+    }
+    Dev &d = *g.devs[0];
+    const uint32_t rows = band_rows_local(height, band_rows, n_parts, part);
+    if (rows && width) render_core(d, width, height, band_rows, n_parts, part, rows, dev_out, st);
     return rows;
 }
 
 // Test hook: drain the device and continue the frame count at `frame_no` (tags above every tag in use
-// keep the slot masks valid), to exercise the tag restart before the uint32 count wraps.
+// keep the completion chain valid), to exercise the tag restart before the uint32 count wraps.
 __attribute__((visibility("default"))) void s3r_debug_set_frame_count(uint32_t frame_no) {
     if (!g.initialized) return;
-    HIPCHECK(hipSetDevice(g.device));
-    restart_tags(frame_no > kTagLimit ? kTagLimit : frame_no);
+    for (Dev *d : g.devs) {
+        HIPCHECK(hipSetDevice(d->device));
+        restart_tags(*d, frame_no > kTagLimit ? kTagLimit : frame_no);
+    }
+    HIPCHECK(hipSetDevice(g.devs[0]->device));
 }
 
 __attribute__((visibility("default"))) int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t height,
                                                                 uint32_t band_rows, uint32_t n_parts, uint32_t part,
                                                                 uint32_t *host_frame, void *stream) {
     if (band_rows == 0 || n_parts == 0 || part >= n_parts || ((!dev_rows || !host_frame) && width && height)) return -1;
-    const uint32_t rows = s3r_band_rows_local(height, band_rows, n_parts, part);
+    const uint32_t rows = band_rows_local(height, band_rows, n_parts, part);
     if (!rows || !width) return rows;
-    if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
+    if (g.initialized) HIPCHECK(hipSetDevice(g.devs[0]->device));
+    else if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
     host_pinned(host_frame, (size_t)width * height * sizeof(uint32_t));
-    hipStream_t st = (hipStream_t)stream;
-    const size_t rowb = (size_t)width * sizeof(uint32_t);
-    // this part's bands: b = part, part + n_parts, ...; all full except perhaps the frame's last band
-    const uint32_t nbands = (height + band_rows - 1) / band_rows, last = nbands - 1u;
-    const uint32_t mine = (nbands > part) ? (nbands - part + n_parts - 1u) / n_parts : 0u;
-    const bool partial_last = (uint64_t)nbands * band_rows > height && last % n_parts == part;
-    const uint32_t full = mine - (partial_last ? 1u : 0u);
-    if (full)
-        HIPCHECK(hipMemcpy2DAsync(host_frame + (size_t)part * band_rows * width, (size_t)n_parts * band_rows * rowb, dev_rows,
-                                  (size_t)band_rows * rowb, (size_t)band_rows * rowb, full, hipMemcpyDeviceToHost, st));
-    if (partial_last)
-        HIPCHECK(hipMemcpyAsync(host_frame + (size_t)last * band_rows * width, dev_rows + (size_t)full * band_rows * width,
-                                (size_t)(height - last * band_rows) * rowb, hipMemcpyDeviceToHost, st));
+    copy_bands_to_host(dev_rows, width, height, band_rows, n_parts, part, host_frame, (hipStream_t)stream);
     return rows;
 }
 
 __attribute__((visibility("default"))) void s3r_unregister_host(void *ptr) {
     if (!ptr) return;
     for (size_t i = g.regs.size(); i-- > 0;) {
-        if (g.regs[i].p != ptr) continue;
+        const uintptr_t a = (uintptr_t)ptr;
+        if (a < g.regs[i].a || a >= g.regs[i].b) continue;
         if (g.regs[i].ok) {
-            if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
-            HIPCHECK(hipDeviceSynchronize());          // no copy into it may still be in flight
-            (void)hipHostUnregister(ptr);
+            if (g.initialized) drain_devices();
+            else {
+                if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
+                HIPCHECK(hipDeviceSynchronize());          // no copy into it may still be in flight
+            }
         }
+        unregister_range(g.regs[i]);
         g.regs.erase(g.regs.begin() + (long)i);
     }
 }
 
+__attribute__((visibility("default"))) int s3r_host_pinned(const void *ptr, uint64_t bytes) {
+    const Lib::Reg *r = ptr ? find_reg(ptr, (size_t)bytes) : nullptr;
+    return r && r->ok ? 1 : 0;
+}
+
+__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[6]) {
+    out[0] = g.pinned_frames;
+    out[1] = g.pageable_frames;
+    out[2] = g.registrations;
+    out[3] = g.merges;
+    out[4] = g.regs.size();
+    out[5] = g.stale_pins;
+}
+
 __attribute__((visibility("default"))) void s3r_timing(int enable) {
     g.timing = enable != 0;
-    g.tcount = 0;
+    for (Dev *d : g.devs) d->tcount = 0;
 }
 
 __attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
     double frag = 0, frame = 0;
-    for (size_t i = 0; i < g.tcount; i++) {
-        float a = 0, b = 0;
-        HIPCHECK(hipEventSynchronize(g.tslots[i].frag1));
-        HIPCHECK(hipEventElapsedTime(&a, g.tslots[i].frag0, g.tslots[i].frag1));
-        HIPCHECK(hipEventElapsedTime(&b, g.tslots[i].frame0, g.tslots[i].frag1));
-        frag += a;
-        frame += b;
+    size_t n = 0;
+    if (!g.devs.empty()) {
+        Dev &d = *g.devs[0];
+        HIPCHECK(hipSetDevice(d.device));
+        for (size_t i = 0; i < d.tcount; i++) {
+            float a = 0, b = 0;
+            HIPCHECK(hipEventSynchronize(d.tslots[i].frag1));
+            HIPCHECK(hipEventElapsedTime(&a, d.tslots[i].frag0, d.tslots[i].frag1));
+            HIPCHECK(hipEventElapsedTime(&b, d.tslots[i].frame0, d.tslots[i].frag1));
+            frag += a;
+            frame += b;
+        }
+        n = d.tcount;
+        for (Dev *e : g.devs) e->tcount = 0;
     }
     out[0] = frag;
     out[1] = frame;
-    out[2] = (double)g.tcount;
-    g.tcount = 0;
+    out[2] = (double)n;
 }
 
 __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
+    const Dev *d = g.devs.empty() ? nullptr : g.devs[0];
     out[0] = g.nv; out[1] = g.nindices; out[2] = g.na; out[3] = g.ntex; out[4] = 2ull * g.ntri;
-    out[5] = g.last_pairs;                   // tile path: (slot, tile) pairs binned last frame
-    out[6] = (uint64_t)g.last_path;          // fragment stage of the last frame: 1 rows, 2 tiles
+    out[5] = d ? d->last_pairs : 0;          // tile path: (slot, tile) pairs binned last frame
+    out[6] = d ? (uint64_t)d->last_path : 0; // fragment stage of the last frame: 1 rows, 2 tiles
     out[7] = g.stale_pins;                   // stale host registrations replaced by updateAndRender
 }
 

@@ -14,7 +14,7 @@ namespace s3r {
 // out[lr * W + x].
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs, uint32_t tag,
+                     uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a

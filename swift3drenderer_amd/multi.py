@@ -63,6 +63,10 @@ class HostFrame:
         import os
         import uuid
         self.rank = rank
+        shared = dist.is_available() and dist.is_initialized()
+        if rank != 0 and not shared:
+            raise RuntimeError('HostFrame: rank != 0 needs an initialised torch.distributed process group '
+                               '(rank 0 creates the shared frame and broadcasts its name)')
         name = [f'/dev/shm/s3r_frame_{os.getpid()}_{uuid.uuid4().hex[:12]}' if rank == 0 else None]
         if dist.is_available() and dist.is_initialized():
             dist.broadcast_object_list(name, src=0, group=group)

@@ -16,8 +16,10 @@ from .abi import Input, pixel_data_for
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 
-EXPORTS = ['updateAndRender', 's3r_configure', 's3r_shutdown', 's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host',
-           's3r_render_bands', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect', 's3r_scene_counts', 's3r_camera']
+EXPORTS = ['updateAndRender', 's3r_configure', 's3r_configure_devices', 's3r_devices', 's3r_shutdown',
+           's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host', 's3r_host_pinned', 's3r_host_stats',
+           's3r_render_bands', 's3r_bands_to_host', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect',
+           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count']
 
 _lib = None
 # host frames of update_and_render(out=None), one per shape, kept for the process: the library may
@@ -58,6 +60,17 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_unregister_host.restype = None
     lib.s3r_debug_set_frame_count.argtypes = [ctypes.c_uint32]
     lib.s3r_debug_set_frame_count.restype = None
+    lib.s3r_configure_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_uint32]
+    lib.s3r_configure_devices.restype = ctypes.c_int
+    lib.s3r_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.s3r_devices.restype = ctypes.c_int
+    lib.s3r_host_pinned.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    lib.s3r_host_pinned.restype = ctypes.c_int
+    lib.s3r_host_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    lib.s3r_host_stats.restype = None
+    missing = [name for name in EXPORTS if not hasattr(lib, name)]
+    if missing:
+        raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
     _lib = lib
     return lib
 
@@ -81,6 +94,28 @@ class Renderer:
 
     def configure(self, data_path: str | None, device: int = -1):
         self.lib.s3r_configure(data_path.encode() if data_path else None, device)
+
+    def configure_devices(self, device_ids, band: int = 0):
+        """updateAndRender over several devices (interleaved row bands, each device copying its rows
+        into the caller's buffer); [] = one device.  Drops all state like configure()."""
+        ids = (ctypes.c_int * max(len(device_ids), 1))(*device_ids)
+        if self.lib.s3r_configure_devices(ids, len(device_ids), band) != 0:
+            raise ValueError(f'bad device list {device_ids!r}')
+
+    def devices(self):
+        out = (ctypes.c_int * 64)()
+        n = self.lib.s3r_devices(out, 64)
+        return list(out[:n])
+
+    def host_pinned(self, arr: np.ndarray) -> bool:
+        """Whether the library holds a successful page-lock covering the array's bytes."""
+        return bool(self.lib.s3r_host_pinned(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
+
+    def host_stats(self) -> dict:
+        out = (ctypes.c_uint64 * 6)()
+        self.lib.s3r_host_stats(out)
+        keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale')
+        return dict(zip(keys, (int(v) for v in out)))
 
     def update_and_render(self, width: int, height: int, inp, out: np.ndarray | None = None) -> np.ndarray:
         """updateAndRender into a host uint32 (H, W) buffer (the reference's contract).
