@@ -114,11 +114,19 @@ void s3r_unregister_host(void *ptr);
  * existing registration -- the second half of the reference's double buffer (one 2 * bufferSize
  * allocation, main.swift:164) shares the seam page with the first -- is merged with it into one
  * registration covering both.  s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful
- * registration.  s3r_host_stats: {frames copied into a pinned buffer, frames copied into a pageable
- * one, successful registrations, registrations merged into a larger one, registrations held, stale
- * registrations replaced}. */
+ * registration.  s3r_host_stats: {frames delivered into a pinned buffer, frames copied into a
+ * pageable one, successful registrations, registrations merged into a larger one, registrations
+ * held, stale registrations replaced, frames delivered by host fill, fill threads}. */
 int s3r_host_pinned(const void *ptr, uint64_t bytes);
-void s3r_host_stats(uint64_t out[6]);
+void s3r_host_stats(uint64_t out[8]);
+
+/* Host-fill delivery (default for the row path into a page-locked buffer): the GPU writes only the
+ * frame's covered bins -- bins some triangle meets -- straight into the caller's buffer, and
+ * `threads` library threads write the background of the sky bins meanwhile (render.cpp:282's fill),
+ * so the PCIe link carries the covered bins only.  threads = 0: every pixel is rendered into device
+ * memory and copied over the link; -1: S3R_FILL_THREADS or the default (8).  Pixels are identical
+ * either way.  Returns 0, or -1 for threads > 64. */
+int s3r_set_fill_threads(int threads);
 
 /* Rows of a height-row frame owned by `part`. */
 uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);

@@ -28,6 +28,9 @@ ARCH = os.environ.get('S3R_ARCH', 'gfx950')
 FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-ffp-contract=off', '-fno-slp-vectorize',
          '-fno-fast-math', '-Wall', '-Wno-unused-function', '-Wno-bitwise-instead-of-logical', f'-I{os.path.join(ROOT, "include")}']
 SOURCES = ['kernels.hip', 'render_api.cpp']
+# host-only C++ (no HIP): compiled by g++ so x86 intrinsics stay out of the HIP compilation
+HOST_SOURCES = ['host_fill.cpp']
+HOST_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-Wall']
 
 
 def _newer(target: str, deps) -> bool:
@@ -53,8 +56,23 @@ def build_variant(tag: str, defines: dict, verbose: bool = False) -> str:
         o = os.path.join(bdir, src + '.o')
         subprocess.run([HIPCC, *FLAGS, *extra, '-x', 'hip', '-c', os.path.join(CSRC, src), '-o', o], check=True)
         objs.append(o)
+    objs += _host_objects(bdir, False)
     subprocess.run([HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', lib_path, '-ldl'], check=True)
     return lib_path
+
+
+def _host_objects(bdir: str, force: bool, verbose: bool = False):
+    objs = []
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(bdir, src + '.o')
+        objs.append(o)
+        if force or not _newer(o, [s]):
+            cmd = ['g++', *HOST_FLAGS, '-c', s, '-o', o]
+            if verbose:
+                print(' '.join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+    return objs
 
 
 def build_library(force: bool = False, verbose: bool = False, stats: bool = False, ablate: int = 0) -> str:
@@ -78,6 +96,7 @@ def build_library(force: bool = False, verbose: bool = False, stats: bool = Fals
             if verbose:
                 print(' '.join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True)
+    objs += _host_objects(bdir, force, verbose)
     if force or not _newer(lib_path, objs):
         cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', lib_path, '-ldl']
         if verbose:

@@ -957,7 +957,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   uint32_t rows_local,
                                                   uint32_t *__restrict__ bincnt,
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
-                                                  uint32_t prev_tag, uint32_t *__restrict__ order) {
+                                                  uint32_t prev_tag, uint32_t *__restrict__ order,
+                                                  uint32_t frame_rows, uint32_t host_fill) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1010,13 +1011,16 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     }
     __syncthreads();
     const uint32_t npairs = sh.cnt;
+    // output row: local row lr of a compact part buffer, or (frame_rows) frame row y of a whole frame
+    const size_t orow = (size_t)(frame_rows ? y : lr) * W;
     if (npairs == 0) {
         // no triangle meets this block (sky): background only (render.cpp:282), 16 B per lane where
-        // the row segment is 16-B aligned
-        if (row_ok) {
-            uint32_t *seg = out + (size_t)lr * W + xs;
+        // the row segment is 16-B aligned -- unless the host fills sky bins (host_fill: the frame is
+        // the caller's host buffer, k_sky_flags told the host which bins are sky)
+        if (row_ok && !host_fill) {
+            uint32_t *seg = out + orow + xs;
             const uint32_t n = xe - xs + 1u;
-            if (((size_t)lr * W + xs) % 4u == 0u) {
+            if ((orow + xs) % 4u == 0u) {
                 const uint4 bg4 = make_uint4(kBackground, kBackground, kBackground, kBackground);
                 for (uint32_t i = lane; i < n / 4u; i += 64u) reinterpret_cast<uint4 *>(seg)[i] = bg4;
                 for (uint32_t i = (n & ~3u) + lane; i < n; i += 64u) seg[i] = kBackground;
@@ -1086,7 +1090,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         r0_sk = st_k[lane];
     }
 
-    uint32_t *row = out + (size_t)lr * W;
+    uint32_t *row = out + orow;
     S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + kChunk * q;
@@ -2006,16 +2010,27 @@ constexpr uint64_t kMinFragBlocks = 2000;   // measured best or near-best for 4K
 // and launches its own frame part (render_api.cpp), and parts may differ in rows
 static thread_local uint32_t g_segch = kSegChunks;
 
-void fragment_configure(uint32_t W, uint32_t rows_local) {
+static uint32_t segment_chunks(uint32_t W, uint32_t rows_local) {
     const char *mb_env = getenv("S3R_MIN_BLOCKS");                                  // tuning / test override
     const uint64_t min_blocks = mb_env ? strtoull(mb_env, nullptr, 10) : kMinFragBlocks;
     const bool try3 = getenv("S3R_SEG3") != nullptr;                                // tuning override
-    g_segch = 1;
     for (uint32_t c : {6u, 3u, 2u}) {
         if (c == 3u && !try3) continue;
         const uint64_t blocks = (uint64_t)((rows_local + kWaves - 1) / kWaves) * ((W + kChunk * c - 1) / (kChunk * c));
-        if (blocks >= min_blocks) { g_segch = c; break; }
+        if (blocks >= min_blocks) return c;
     }
+    return 1u;
+}
+
+void fragment_configure(uint32_t W, uint32_t rows_local) { g_segch = segment_chunks(W, rows_local); }
+
+FragLayout fragment_layout(uint32_t W, uint32_t rows_local) {
+    FragLayout l;
+    l.seg_px = kChunk * segment_chunks(W, rows_local);
+    l.segs = (W + l.seg_px - 1) / l.seg_px;
+    l.rows_per_bin = kWaves;
+    l.bins = (uint64_t)((rows_local + kWaves - 1) / kWaves) * l.segs;
+    return l;
 }
 
 uint32_t fragment_segment_pixels() { return kChunk * g_segch; }
@@ -2047,7 +2062,8 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
-                     hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order) {
+                     hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
+                     bool frame_rows, bool host_fill) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2061,10 +2077,40 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order);
+                              done_flag, prev_tag, order, (uint32_t)frame_rows, (uint32_t)host_fill);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
-                           W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order);
+                           W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
+                           (uint32_t)frame_rows, (uint32_t)host_fill);
+}
+
+// Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in
+// host-coherent memory -- tag, with kSkyBit when no triangle meets the bin -- so the host writes the
+// background of sky bins while k_fragment writes only the covered bins into the caller's buffer.
+// probe (may be null): the device address of the caller's pixel 0; the magic written there before
+// bin 0's flag (release) lets the host check that the mapping reaches the caller's pages.
+__global__ void __launch_bounds__(256) k_sky_flags(const uint32_t *__restrict__ bincnt, uint32_t nbins, uint32_t *flags,
+                                                   uint32_t tag, uint32_t *probe) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    if (b >= nbins) return;
+    const uint32_t f = bincnt[b] == 0u ? (tag | kSkyBit) : tag;
+    if (b == 0 && probe) {
+        __hip_atomic_store(probe, kMapProbe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(flags, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        __hip_atomic_store(flags + b, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, uint32_t tag, uint32_t *probe,
+                      hipStream_t st, hipEvent_t done) {
+    const uint32_t blocks = (uint32_t)((nbins + 255) / 256);
+    if (blocks == 0) {
+        if (done) (void)hipEventRecord(done, st);
+        return;
+    }
+    hipExtLaunchKernelGGL(k_sky_flags, dim3(blocks), dim3(256), 0, st, nullptr, done, 0, bincnt, (uint32_t)nbins, flags,
+                          tag, probe);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

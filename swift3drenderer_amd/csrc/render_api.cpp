@@ -36,6 +36,11 @@
 #include "../../include/render.h"
 #include "s3r_kernels.h"
 
+namespace s3r_host {   // host_fill.cpp
+void fill_words(uint32_t *p, size_t n, uint32_t v);
+void store_fence();
+}
+
 using namespace s3r;
 
 #define HIPCHECK(x)                                                                                   \
@@ -136,6 +141,13 @@ struct Dev {
     std::vector<TimingSlot> tslots;
     size_t tcount = 0;
     HostProf hp;
+    // host fill: one flag per fragment bin (host-coherent; k_sky_flags), this device's tag sequence,
+    // and the device address of the caller-buffer registration the last host-fill frame used
+    uint32_t *fill_flags = nullptr, *fill_flags_dev = nullptr;
+    uint64_t fill_cap = 0;
+    uint32_t fill_tag = 0;
+    uintptr_t map_host = 0, map_dev = 0;
+    uint64_t map_epoch = 0;
 };
 
 // The scene as read from data.bin (render.cpp:177-209), converted to the device layout once and
@@ -171,26 +183,34 @@ class Pool {
         for (auto &t : th_) t.join();
         th_.clear();
     }
-    void run(void (*fn)(void *, int), void *arg, int n) {
-        if (n > 1) {
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                fn_ = fn;
-                arg_ = arg;
-                active_ = n;
-                pending_.store(n - 1, std::memory_order_relaxed);
-                gen_.fetch_add(1, std::memory_order_release);
-            }
-            cv_work_.notify_all();
+    // fn(arg, i) on workers 0 < i < n, asynchronously; join() waits for them
+    void launch(void (*fn)(void *, int), void *arg, int n) {
+        launched_ = n > 1;
+        if (!launched_) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = fn;
+            arg_ = arg;
+            active_ = n;
+            pending_.store(n - 1, std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
         }
-        fn(arg, 0);
-        if (n > 1) {
-            if (!spin([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
-            }
+        cv_work_.notify_all();
+    }
+    void join() {
+        if (!launched_) return;
+        launched_ = false;
+        if (!spin([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
         }
     }
+    void run(void (*fn)(void *, int), void *arg, int n) {
+        launch(fn, arg, n);
+        fn(arg, 0);
+        join();
+    }
+    int workers() const { return (int)th_.size(); }
     ~Pool() { stop(); }
 
   private:
@@ -234,6 +254,7 @@ class Pool {
     void (*fn_)(void *, int) = nullptr;
     void *arg_ = nullptr;
     int active_ = 0;
+    bool launched_ = false;
 };
 
 struct Lib {
@@ -270,6 +291,13 @@ struct Lib {
     std::vector<Reg> regs;
     uint64_t stale_pins = 0;                   // registrations found stale and replaced (updateAndRender)
     uint64_t pinned_frames = 0, pageable_frames = 0, registrations = 0, merges = 0;
+    uint64_t reg_epoch = 1;                    // bumped whenever a registration goes away
+
+    // host fill (updateAndRender, row path): the GPU writes covered bins straight into the caller's
+    // page-locked buffer, fill_threads library threads write the sky bins' background meanwhile
+    int fill_threads = -1;                     // -1: S3R_FILL_THREADS or the default; 0: off
+    Pool fill_pool;
+    uint64_t host_fill_frames = 0;
 };
 
 Lib g;
@@ -502,6 +530,7 @@ void unregister_all() {
     for (auto &r : g.regs)
         if (r.ok) (void)hipHostUnregister((void *)r.a);
     g.regs.clear();
+    g.reg_epoch++;
 }
 
 void dev_release(Dev &d) {
@@ -518,6 +547,7 @@ void dev_release(Dev &d) {
     if (d.done_host) (void)hipHostFree((void *)d.done_host);
     if (d.handoff) (void)hipEventDestroy(d.handoff);
     if (d.tile_total_host) (void)hipHostFree(d.tile_total_host);
+    if (d.fill_flags) (void)hipHostFree(d.fill_flags);
     for (int p = 0; p < kSets; p++) {
         if (d.geo_done[p]) (void)hipEventDestroy(d.geo_done[p]);
         if (d.frag_done[p]) (void)hipEventDestroy(d.frag_done[p]);
@@ -532,6 +562,7 @@ void dev_release(Dev &d) {
 
 void release_all() {
     g.pool.stop();
+    g.fill_pool.stop();
     if (g.initialized) {
         for (Dev *d : g.devs) {
             (void)hipSetDevice(d->device);
@@ -550,8 +581,10 @@ void release_all() {
     const int dev = g.device, rp = g.raster_path;
     const std::vector<int> ids = g.device_ids;
     const uint32_t band = g.band_rows;
+    const int fill = g.fill_threads;
     g.~Lib();
     new (&g) Lib();
+    g.fill_threads = fill;
     g.data_path = path;
     g.device = dev;
     g.raster_path = rp;
@@ -739,10 +772,15 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     HIPCHECK(hipGetLastError());
 }
 
+// Host fill for one frame part: the flags the sky-flag kernel writes (device address) and the tag.
+struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; };
+
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
-// band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.
+// band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
+// (row path only) `out` is the whole W x H frame in the caller's mapped host buffer: the fragment
+// kernel writes this part's covered bins at their frame rows and leaves the sky bins to the host.
 void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                 uint32_t *out, hipStream_t st) {
+                 uint32_t *out, hipStream_t st, const HostFill *hf = nullptr) {
     TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
         render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts);
@@ -804,8 +842,11 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     d.hp.lap(2);
     const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, d.geo_done[p],
+                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, hf ? nullptr : d.geo_done[p],
                     lpt ? d.order[p] : nullptr);
+    // host fill: the bins' sky flags to the host as soon as the counts are final (before the
+    // fragment kernel, which resets the counts, may start)
+    if (hf) launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, d.geo_done[p]);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
@@ -817,7 +858,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
-                    lpt ? d.order[p] : nullptr);
+                    lpt ? d.order[p] : nullptr, hf != nullptr, hf != nullptr);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -842,6 +883,7 @@ Lib::Reg *find_reg(const void *p, size_t n) {
 
 void unregister_range(Lib::Reg &r) {
     if (r.ok) (void)hipHostUnregister((void *)r.a);
+    g.reg_epoch++;
 }
 
 // Page-lock [p, p + n) for DMA (cached).  The request is widened to whole pages; registrations it
@@ -866,7 +908,8 @@ bool host_pinned(void *p, size_t n) {
         g.merges++;
     }
     if (g.regs.size() >= 4) unregister_all();
-    const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable) == hipSuccess;
+    // mapped: the host-fill delivery has the GPU write covered bins straight into these pages
+    const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;
     if (!ok) (void)hipGetLastError();
     else g.registrations++;
     g.regs.push_back({a, b, ok});
@@ -970,6 +1013,174 @@ void deliver_part(void *arg, int i) {
     HIPCHECK(hipStreamSynchronize(d.stream));
 }
 
+// ---------------------------------------------------------------- host-fill delivery
+// updateAndRender's PCIe link carries every pixel of the frame in the copy delivery above, although
+// typically half the frame's bins are sky -- bins no triangle meets, all background (render.cpp:282).
+// Host fill: each device writes only its covered bins, straight into their rows of the caller's
+// mapped, page-locked buffer (k_fragment frame_rows + host_fill), and publishes every bin's sky flag
+// as soon as its geometry is done (k_sky_flags); meanwhile the library's fill threads write the sky
+// bins' background with streaming stores.  The link carries the covered bins only, and the host's
+// memory writes overlap the GPU's.
+constexpr int kDefaultFillThreads = 8;
+constexpr uint32_t kFillBlock = 8;            // bins per fill-thread work block (contiguous: whole lines)
+
+int fill_threads() {
+    if (g.fill_threads < 0) {
+        const char *e = getenv("S3R_FILL_THREADS");
+        const int v = e ? atoi(e) : kDefaultFillThreads;
+        g.fill_threads = v < 0 ? 0 : (v > 64 ? 64 : v);
+    }
+    return g.fill_threads;
+}
+
+struct FillPart {
+    uint32_t *flags;                 // host view of the device's flags
+    uint32_t tag, seg_px, segs, rpb, rows_local, band, nparts, part;
+    uint64_t bins;
+};
+
+struct FillJob {
+    uint32_t *frame;                 // the caller's buffer (host address)
+    uint32_t W, H;
+    int nparts, threads;
+    FillPart parts[kMaxDevices];
+    HostFill hf[kMaxDevices];
+    std::atomic<bool> stale{false};  // pixel 0 checked before its bin was filled: the mapping is stale
+};
+
+void fill_bin(const FillJob &job, const FillPart &fp, uint64_t b) {
+    const uint32_t blk = (uint32_t)(b / fp.segs), seg = (uint32_t)(b % fp.segs);
+    const uint32_t xs = seg * fp.seg_px, xe = xs + fp.seg_px < job.W ? xs + fp.seg_px : job.W;
+    for (uint32_t k = 0; k < fp.rpb; k++) {
+        const uint32_t lr = blk * fp.rpb + k;
+        if (lr >= fp.rows_local) break;
+        const uint32_t y = ((lr / fp.band) * fp.nparts + fp.part) * fp.band + lr % fp.band;
+        if (y >= job.H) continue;
+        s3r_host::fill_words(job.frame + (size_t)y * job.W + xs, xe - xs, kBackground);
+    }
+}
+
+// Fill thread idx (1..threads): the blocks of kFillBlock bins it owns in every part, each handled as
+// soon as its flags carry this frame's tag -- sky bins filled, covered ones left to the GPU.
+void fill_worker(void *arg, int idx) {
+    FillJob &job = *static_cast<FillJob *>(arg);
+    const uint64_t t = (uint64_t)idx - 1, T = (uint64_t)job.threads;
+    thread_local std::vector<uint64_t> pend;
+    pend.clear();
+    for (int p = 0; p < job.nparts; p++)
+        for (uint64_t b = t * kFillBlock; b < job.parts[p].bins; b += T * kFillBlock)
+            for (uint64_t k = b; k < b + kFillBlock && k < job.parts[p].bins; k++) pend.push_back((uint64_t)p << 48 | k);
+    size_t n = pend.size();
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t idle = 0;
+    while (n) {
+        size_t keep = 0;
+        for (size_t i = 0; i < n; i++) {
+            const uint64_t e = pend[i];
+            const FillPart &fp = job.parts[e >> 48];
+            const uint64_t b = e & 0xFFFFFFFFFFFFull;
+            const uint32_t f = __atomic_load_n(fp.flags + b, __ATOMIC_ACQUIRE);
+            if ((f & ~kSkyBit) != fp.tag) { pend[keep++] = e; continue; }
+            if (!(f & kSkyBit)) continue;
+            // pixel 0's bin: the sky-flag kernel wrote kMapProbe there through its mapping first
+            if ((e >> 48) == 0 && b == 0 && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
+                job.stale.store(true, std::memory_order_relaxed);
+            fill_bin(job, fp, b);
+        }
+        if (keep == n) {
+            __builtin_ia32_pause();
+            if ((++idle & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
+                fprintf(stderr, "s3r: host fill: %zu bins never flagged (device fault?)\n", keep);
+                abort();
+            }
+        }
+        n = keep;
+    }
+    s3r_host::store_fence();
+}
+
+// The device address of host buffer p inside registration r on device d (cached per registration).
+uint32_t *mapped_ptr(Dev &d, const Lib::Reg &r, void *p) {
+    if (d.map_epoch != g.reg_epoch || d.map_host != r.a) {
+        void *dp = nullptr;
+        HIPCHECK(hipHostGetDevicePointer(&dp, (void *)r.a, 0));
+        d.map_host = r.a;
+        d.map_dev = (uintptr_t)dp;
+        d.map_epoch = g.reg_epoch;
+    }
+    return (uint32_t *)(d.map_dev + ((uintptr_t)p - r.a));
+}
+
+struct DirectDelivery {
+    FillJob *job;
+    const Lib::Reg *reg;
+};
+
+// Part i of a host-fill frame on device i: render its covered bins into the caller's mapped buffer.
+void deliver_part_direct(void *arg, int i) {
+    const DirectDelivery &dd = *static_cast<const DirectDelivery *>(arg);
+    FillJob &job = *dd.job;
+    Dev &d = *g.devs[i];
+    HIPCHECK(hipSetDevice(d.device));
+    const FillPart &fp = job.parts[i];
+    if (fp.rows_local && job.W) {
+        uint32_t *frame_dev = mapped_ptr(d, *dd.reg, job.frame);
+        HostFill hf = job.hf[i];
+        hf.probe_dev = i == 0 ? frame_dev : nullptr;
+        render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf);
+    }
+    HIPCHECK(hipStreamSynchronize(d.stream));
+}
+
+// One updateAndRender frame by host fill.  Returns false if the caller's registration turned out to
+// be stale (the frame did not reach the caller's pages: the caller redoes it by copy).
+bool host_fill_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts) {
+    const Lib::Reg *reg = find_reg(buffer, (size_t)W * H * 4);
+    FillJob job;
+    job.frame = buffer;
+    job.W = W;
+    job.H = H;
+    job.nparts = (int)nparts;
+    job.threads = fill_threads();
+    const uint32_t band = nparts == 1 ? H : g.band;
+    for (uint32_t i = 0; i < nparts; i++) {
+        Dev &d = *g.devs[i];
+        FillPart &fp = job.parts[i];
+        fp.rows_local = nparts == 1 ? H : band_rows_local(H, band, nparts, i);
+        const FragLayout l = fragment_layout(W, fp.rows_local);
+        fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.bins = fp.rows_local ? l.bins : 0;
+        fp.band = band; fp.nparts = nparts; fp.part = i;
+        if (d.fill_cap < fp.bins) {
+            HIPCHECK(hipSetDevice(d.device));
+            if (d.fill_flags) HIPCHECK(hipHostFree(d.fill_flags));
+            HIPCHECK(hipHostMalloc((void **)&d.fill_flags, fp.bins * sizeof(uint32_t),
+                                   hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+            memset(d.fill_flags, 0, fp.bins * sizeof(uint32_t));
+            HIPCHECK(hipHostGetDevicePointer((void **)&d.fill_flags_dev, d.fill_flags, 0));
+            d.fill_cap = fp.bins;
+            d.fill_tag = 0;
+        }
+        if (++d.fill_tag >= kSkyBit) {                 // (after 2^31 frames) restart the tags
+            memset(d.fill_flags, 0, d.fill_cap * sizeof(uint32_t));
+            d.fill_tag = 1;
+        }
+        fp.flags = d.fill_flags;
+        fp.tag = d.fill_tag;
+        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr};
+    }
+    HIPCHECK(hipSetDevice(g.devs[0]->device));
+    buffer[0] = kStaleProbe;                          // k_sky_flags overwrites it via the mapping
+    DirectDelivery dd{&job, reg};
+    g.fill_pool.launch(fill_worker, &job, job.threads + 1);
+    g.pool.run(deliver_part_direct, &dd, (int)nparts);
+    g.fill_pool.join();
+    // pixel 0 in a covered bin: the GPU wrote it (a pixel, neither probe) unless the mapping is stale
+    const uint32_t f0 = job.parts[0].bins ? job.parts[0].flags[0] : 0;
+    const bool stale = job.stale.load() || (!(f0 & kSkyBit) && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
+    g.host_fill_frames++;
+    return !stale;
+}
+
 }  // namespace
 
 extern "C" {
@@ -988,8 +1199,22 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     const uint32_t nparts = (ndev > 1 && copy_bytes == frame_bytes && H > g.band) ? ndev : 1u;
     Delivery job{W, H, g.band, nparts, pixel_data->buffer, copy_bytes, false};
     bool pinned = false;
-    if (copy_bytes) {
+    if (copy_bytes) pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+    if (pinned && npx && copy_bytes == frame_bytes && fill_threads() > 0 && !use_tile_path()) {
+        // host fill: covered bins by the GPU(s) straight into the buffer, sky bins by the host
+        if (g.fill_pool.workers() != g.fill_threads) g.fill_pool.start(g.fill_threads);
+        if (host_fill_frame(pixel_data->buffer, W, H, nparts)) {
+            g.pinned_frames++;
+            for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
+            HIPCHECK(hipSetDevice(g.devs[0]->device));
+            return;
+        }
+        // the registration no longer maps the caller's pages: pin anew, render the frame by copy
+        drop_registration(pixel_data->buffer, pixel_data->bufferSize);
+        g.stale_pins++;
         pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+    }
+    if (copy_bytes) {
         if (pinned && copy_words) stamp_probes(pixel_data->buffer, copy_words);
         (pinned ? g.pinned_frames : g.pageable_frames)++;
     }
@@ -1119,13 +1344,22 @@ __attribute__((visibility("default"))) int s3r_host_pinned(const void *ptr, uint
     return r && r->ok ? 1 : 0;
 }
 
-__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[6]) {
+__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[8]) {
     out[0] = g.pinned_frames;
     out[1] = g.pageable_frames;
     out[2] = g.registrations;
     out[3] = g.merges;
     out[4] = g.regs.size();
     out[5] = g.stale_pins;
+    out[6] = g.host_fill_frames;
+    out[7] = (uint64_t)fill_threads();
+}
+
+__attribute__((visibility("default"))) int s3r_set_fill_threads(int threads) {
+    if (threads > 64) return -1;
+    g.fill_pool.stop();
+    g.fill_threads = threads < 0 ? -1 : threads;
+    return 0;
 }
 
 __attribute__((visibility("default"))) void s3r_timing(int enable) {

@@ -10,12 +10,15 @@ namespace s3r {
 // costs; the fragment launch reads perm and stores each bin's time into cost, for the next frame
 // on the same buffer set (a hint only: any permutation renders the same pixels).
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
-// (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact:
-// out[lr * W + x].
+// (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact,
+// out[lr * W + x], or with frame_rows the whole frame's row, out[y * W + x] (out = a W x H frame, e.g.
+// the caller's host buffer).  host_fill: sky bins (no triangle) write nothing -- the host fills them
+// (launch_sky_flags).
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
-                     hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order);
+                     hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
+                     bool frame_rows = false, bool host_fill = false);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
 // pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0
@@ -41,6 +44,22 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
+
+// The row path's fragment bins for a frame part of W x rows_local (what fragment_configure picks):
+// bin b covers local rows (b / segs) * rows_per_bin ... + rows_per_bin - 1, columns
+// (b % segs) * seg_px ... + seg_px - 1 (clipped to the part and the frame).
+struct FragLayout { uint32_t seg_px, segs, rows_per_bin; uint64_t bins; };
+FragLayout fragment_layout(uint32_t W, uint32_t rows_local);
+
+// Host fill: flags[b] = tag | (kSkyBit if bin b has no pair) for the bins' counts of the geometry
+// just launched on st (system-scope stores into host-coherent memory); `done` recorded on completion.
+// probe (may be null): device address of the caller's pixel 0, set to kMapProbe before flags[0] is
+// published (the host's check that the mapping of its buffer is not stale).  Neither value is a
+// pixel (pixels are 0x00RRGGBB).
+constexpr uint32_t kSkyBit = 0x80000000u;
+constexpr uint32_t kMapProbe = 0xFEA5A5A5u;
+void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, uint32_t tag, uint32_t *probe,
+                      hipStream_t st, hipEvent_t done);
 // Picks the row path's segment width for a frame of W x rows_local; call before the helpers above.
 void fragment_configure(uint32_t W, uint32_t rows_local);
 

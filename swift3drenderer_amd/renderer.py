@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 EXPORTS = ['updateAndRender', 's3r_configure', 's3r_configure_devices', 's3r_devices', 's3r_shutdown',
            's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host', 's3r_host_pinned', 's3r_host_stats',
            's3r_render_bands', 's3r_bands_to_host', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect',
-           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count']
+           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_fill_threads']
 
 _lib = None
 # host frames of update_and_render(out=None), one per shape, kept for the process: the library may
@@ -68,6 +68,8 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_host_pinned.restype = ctypes.c_int
     lib.s3r_host_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_host_stats.restype = None
+    lib.s3r_set_fill_threads.argtypes = [ctypes.c_int]
+    lib.s3r_set_fill_threads.restype = ctypes.c_int
     missing = [name for name in EXPORTS if not hasattr(lib, name)]
     if missing:
         raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
@@ -112,10 +114,17 @@ class Renderer:
         return bool(self.lib.s3r_host_pinned(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
 
     def host_stats(self) -> dict:
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 8)()
         self.lib.s3r_host_stats(out)
-        keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale')
+        keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale', 'host_fill_frames',
+                'fill_threads')
         return dict(zip(keys, (int(v) for v in out)))
+
+    def set_fill_threads(self, threads: int):
+        """Host-fill delivery with `threads` fill threads (0: copy every pixel over the link; -1: the
+        S3R_FILL_THREADS / default)."""
+        if self.lib.s3r_set_fill_threads(int(threads)) != 0:
+            raise ValueError(f'bad fill thread count {threads}')
 
     def update_and_render(self, width: int, height: int, inp, out: np.ndarray | None = None) -> np.ndarray:
         """updateAndRender into a host uint32 (H, W) buffer (the reference's contract).

@@ -160,3 +160,38 @@ def test_parts_pin_the_callers_double_buffer(multi, scene_dir):
     frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', w, h, extra=6), [0] * 4)
     st = multi.host_stats()
     assert st['pageable_frames'] == 0 and st['pinned_frames'] >= 9, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('fill', [0, 1, 3, 16])
+@pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
+def test_delivery_modes_match_oracle(multi, scene_dir, fill, devices):
+    """Both deliveries of updateAndRender -- every pixel rendered into HBM and copied over the link
+    (fill 0), or covered bins written by the GPU straight into the caller's buffer while `fill` host
+    threads write the sky bins (render_api.cpp host fill) -- give the oracle's frames, on one device
+    and on three parts, at 4K (384-px bins) and 1080p (128-px bins)."""
+    try:
+        multi.set_fill_threads(fill)
+        before = multi.host_stats()['host_fill_frames'] if fill else 0
+        frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', 1920, 1080), devices)
+        frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_id', 3840, 2160, extra=1), devices)
+        st = multi.host_stats()
+        assert st['fill_threads'] == fill
+        if fill:
+            assert st['host_fill_frames'] > before
+        else:
+            assert st['host_fill_frames'] == 0
+    finally:
+        multi.set_fill_threads(-1)
+
+
+@pytest.mark.gpu
+def test_host_fill_sparse_and_empty_frames(multi, scene_dir, tmp_path):
+    """Host fill when nothing is visible (every bin sky) and when the scene is empty."""
+    from swift3drenderer_amd import scene
+    empty = str(tmp_path / 'empty.bin')
+    scene.write_scene(scene.Scene(), empty)
+    frames_vs_oracle(multi, empty, pose_frames('P_over', 640, 480), [0])
+    away = [(640, 480, (0, 0, 0, 0, 0, 0)), (640, 480, (0, 0, 0, 0, 4000.0, 0.0)), (640, 480, (0, 0, 0, 0, 8000.0, 0.0))]
+    frames_vs_oracle(multi, scene_dir['full'], away, [0, 0])
+    assert multi.host_stats()['host_fill_frames'] > 0
