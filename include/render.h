@@ -110,10 +110,9 @@ int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t hei
 void s3r_unregister_host(void *ptr);
 
 /* Host buffers.  updateAndRender page-locks the caller's buffer (hipHostRegister, cached) so the
- * frame's copy runs at the pinned DMA rate.  Registrations are whole pages; a buffer overlapping an
- * existing registration -- the second half of the reference's double buffer (one 2 * bufferSize
- * allocation, main.swift:164) shares the seam page with the first -- is merged with it into one
- * registration covering both.  s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful
+ * frame's copy runs at the pinned DMA rate.  A buffer sharing a page with an existing registration
+ * -- the second half of the reference's double buffer (one 2 * bufferSize allocation, main.swift:164)
+ * shares the seam page with the first -- is merged with it into one registration covering both.  s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful
  * registration.  s3r_host_stats: {frames delivered into a pinned buffer, frames copied into a
  * pageable one, successful registrations, registrations merged into a larger one, registrations
  * held, stale registrations replaced, frames delivered by host fill, fill threads}. */

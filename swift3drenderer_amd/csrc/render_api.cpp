@@ -284,9 +284,9 @@ struct Lib {
     Pool pool;
 
     // caller buffers registered as pinned memory (the double buffer: main.swift:117-118, :164):
-    // page-aligned, disjoint ranges [a, b); a request overlapping existing ranges is merged with them
-    // into one registration, so two halves of one allocation -- which share the page at the seam --
-    // end up in one registration that covers both
+    // byte ranges [a, b) whose pages do not overlap; a request whose pages overlap existing ranges is
+    // merged with them into one registration, so two halves of one allocation -- which share the
+    // page at the seam -- end up in one registration that covers both
     struct Reg { uintptr_t a, b; bool ok; };
     std::vector<Reg> regs;
     uint64_t stale_pins = 0;                   // registrations found stale and replaced (updateAndRender)
@@ -886,20 +886,25 @@ void unregister_range(Lib::Reg &r) {
     g.reg_epoch++;
 }
 
-// Page-lock [p, p + n) for DMA (cached).  The request is widened to whole pages; registrations it
-// overlaps -- the other half of a double buffer shares the seam page -- are dropped (after draining
-// the devices) and re-registered as one range covering the union, so each half of the reference's
-// double buffer lies inside ONE registration and its copy runs at the pinned rate.
+// Page-lock [p, p + n) for DMA (cached).  Registrations whose pages the request's pages overlap --
+// the other half of a double buffer shares the seam page -- are dropped (after draining the devices)
+// and re-registered as one range covering the union, so each half of the reference's double buffer
+// lies inside ONE registration and its copy runs at the pinned rate.
 bool host_pinned(void *p, size_t n) {
     if (Lib::Reg *r = find_reg(p, n)) return r->ok;
     if (getenv("S3R_NO_PIN")) return false;
+    // merged when the page ranges overlap (the driver pins whole pages), but the registered range is
+    // the exact byte union of the caller's buffers: a page-rounded one would also cover bytes of a
+    // neighbouring allocation, and a copy into that allocation straddling the registration's end is
+    // then refused by the runtime
     const size_t pg = page_size();
-    uintptr_t a = (uintptr_t)p & ~(uintptr_t)(pg - 1);
-    uintptr_t b = ((uintptr_t)p + n + pg - 1) & ~(uintptr_t)(pg - 1);
+    auto page_lo = [&](uintptr_t x) { return x & ~(uintptr_t)(pg - 1); };
+    auto page_hi = [&](uintptr_t x) { return (x + pg - 1) & ~(uintptr_t)(pg - 1); };
+    uintptr_t a = (uintptr_t)p, b = (uintptr_t)p + n;
     bool drained = false;
     for (size_t i = g.regs.size(); i-- > 0;) {
         Lib::Reg &r = g.regs[i];
-        if (r.b <= a || b <= r.a) continue;
+        if (page_hi(r.b) <= page_lo(a) || page_hi(b) <= page_lo(r.a)) continue;
         if (r.ok && !drained) { drain_devices(); drained = true; }
         a = a < r.a ? a : r.a;
         b = b > r.b ? b : r.b;
