@@ -39,6 +39,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = 'frames/sec + Mpixels/s at 3840x2160, data.bin scene; 1/2/4/8-GPU scaling'
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md, HBM3E peak (spec)
+LINK_PEAK_GBS = 63.0     # MI355X_MICROARCH.md, host link PCIe Gen5 x16 per direction (spec)
 TRI_SETUP_BYTES = 240    # sizeof(TriSetup)
 RASTER_REC_BYTES = 64    # sizeof(RasterRec), tile path
 MIN_TIMED = 200          # >= 200 frames after 20 warm-up frames
@@ -221,34 +222,57 @@ def run_rank0(a, N, np, torch):
     # both halves carry the held pose's frame; the pin state the frames were delivered with
     host = r.host_stats()
     halves_pinned = [bool(lib.s3r_host_pinned(ctypes.c_void_p(buf.ptr + k * buf.size), buf.size)) for k in (0, 1)]
+    used = [m for m in ('copy', 'direct', 'fill') if host[f'{m}_frames'] > 0]
+    link_bytes = host['link_bytes']
 
-    # fragment-kernel time on device 0's stream (HIP events), in a separate pass of the same calls
+    def timed_calls(n):
+        t = np.empty(n)
+        for k in range(n):
+            t0 = clock()
+            uar(refs[buf.cur], in_ref)
+            t[k] = clock() - t0
+            buf.cur ^= 1
+        return t
+
+    # the same calls through each delivery into the caller's buffer (render_api.cpp "deliveries")
+    modes = {}
+    nm = min(steps, 100)
+    for mode in ('copy', 'direct', 'fill'):
+        r.set_delivery(mode)
+        timed_calls(10)
+        tm = timed_calls(nm)
+        hs = r.host_stats()
+        modes[mode] = {'fps': round(1.0 / float(np.median(tm)), 3), 'median_ms': round(float(np.median(tm)) * 1e3, 5),
+                       'link_bytes_per_frame': hs['link_bytes']}
+    r.set_delivery('env')
+    timed_calls(10)
+
+    # fragment-kernel time on device 0's stream (HIP events) within the delivered frames, in a
+    # separate pass of the same calls (with direct / host-fill delivery its stores cross the link)
     r.timing(True)
     nt = min(steps, MIN_TIMED)
     for _ in range(nt):
         call(hold_in)
-    frag_ms, frame_ms, nfr = r.timing_collect()
+    dl_frag_ms, dl_frame_ms, dl_nfr = r.timing_collect()
     r.timing(False)
 
     counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
     nv, ni, na, ntex, nslots, pairs, path = counts[:7]
     rows0 = r.lib.s3r_band_rows_local(H, B, len(devices), 0) if len(devices) > 1 and H > B else H
-    if path == 2:
-        # tile path, fragment stage = k_tile_raster + k_tile_resolve: framebuffer rows, the per-pixel
-        # (1/z, slot) keys written and read back, and per (slot, tile) pair its list entry + 64-B record
-        kernel = 'k_tile_raster+k_tile_resolve'
-        frag_bytes = 4 * W * rows0 + 16 * W * rows0 + (4 + RASTER_REC_BYTES) * pairs
-    else:
-        # row path, k_fragment: device 0's framebuffer rows + the ripmap texels it may sample + the
-        # triangle setup records it reads
-        kernel = 'k_fragment'
-        frag_bytes = 4 * W * rows0 + 4 * ntex + TRI_SETUP_BYTES * nslots
-    frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
-    achieved = frag_bytes / frag_avg_s / 1e9
-    workload = f'{a.scene}/{a.pose}/{W}x{H}/N{len(devices)}'
 
-    # device-resident rate of one GPU: whole frames pipelined into HBM (no host copy)
+    def kernel_bytes(rows):
+        if path == 2:
+            # tile path, fragment stage = k_tile_raster + k_tile_resolve: framebuffer rows, the per-pixel
+            # (1/z, slot) keys written and read back, and per (slot, tile) pair its list entry + 64-B record
+            return 'k_tile_raster+k_tile_resolve', 4 * W * rows + 16 * W * rows + (4 + RASTER_REC_BYTES) * pairs
+        # row path, k_fragment: the framebuffer rows + the ripmap texels it may sample + the triangle
+        # setup records it reads
+        return 'k_fragment', 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
+
+    # device-resident rate of one GPU: whole frames pipelined into HBM (no host copy), and the HBM
+    # roofline of the fragment kernel from HIP events on its stream in a second pass of those frames
     device_fps = None
+    frag_ms, frame_ms, nfr, roof_rows, roof_launch = dl_frag_ms, dl_frame_ms, dl_nfr, rows0, 'delivered frames'
     if not a.no_device:
         r.configure_devices([], B)
         r.configure(data_path, devices[0])
@@ -264,7 +288,17 @@ def run_rank0(a, N, np, torch):
             r.render_bands(hold_in, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize(dev)
         device_fps = steps / (time.perf_counter() - t0)
+        r.timing(True)
+        for _ in range(nt):
+            r.render_bands(hold_in, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
+        frag_ms, frame_ms, nfr = r.timing_collect()
+        r.timing(False)
+        roof_rows, roof_launch = H, 'whole frame into HBM, frames pipelined (device_fps pass)'
         del out
+    kernel, frag_bytes = kernel_bytes(roof_rows)
+    frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
+    achieved = frag_bytes / frag_avg_s / 1e9
+    workload = f'{a.scene}/{a.pose}/{W}x{H}/N1'
 
     cpu = None
     if not a.no_cpu_baseline and len(devices) == 1:
@@ -301,16 +335,24 @@ def run_rank0(a, N, np, torch):
         'p10_ms': round(float(np.percentile(per, 10)) * 1e3, 5),
         'p90_ms': round(float(np.percentile(per, 90)) * 1e3, 5),
         'fps_mean': round(steps / total, 3),
-        'delivery_GB_per_s': round(frame_bytes / median_s / 1e9, 3),
+        'frame_GB_per_s': round(frame_bytes / median_s / 1e9, 3),
+        'delivery': {'mode': used[0] if len(used) == 1 else used, 'fill_threads': host['fill_threads'],
+                     'link_bytes_per_frame': link_bytes, 'modes': modes},
+        'link_roofline': {'bound': 'pcie', 'achieved': round(link_bytes / median_s / 1e9, 2),
+                          'peak': LINK_PEAK_GBS * len(devices), 'unit': 'GB/s',
+                          'frac': round(link_bytes / median_s / 1e9 / (LINK_PEAK_GBS * len(devices)), 5),
+                          'note': 'bytes the devices sent over their host links per frame / median frame time; '
+                                  f'{len(devices)} x PCIe Gen5 x16'},
         'host_buffer': {'halves_pinned': halves_pinned, 'pinned_frames': host['pinned_frames'],
                         'pageable_frames': host['pageable_frames']},
         'device_fps': round(device_fps, 3) if device_fps else None,
         'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
         'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
+        'fragment_kernel_ms_delivered': round(dl_frag_ms / max(dl_nfr, 1), 5),
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
                      'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,
-                     'launch': f'device 0 part ({rows0} of {H} rows) during the updateAndRender frames'},
+                     'launch': roof_launch},
         'cpu_baseline': cpu,
     }
 

@@ -110,22 +110,31 @@ int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t hei
 void s3r_unregister_host(void *ptr);
 
 /* Host buffers.  updateAndRender page-locks the caller's buffer (hipHostRegister, cached) so the
- * frame's copy runs at the pinned DMA rate.  A buffer sharing a page with an existing registration
- * -- the second half of the reference's double buffer (one 2 * bufferSize allocation, main.swift:164)
- * shares the seam page with the first -- is merged with it into one registration covering both.  s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful
- * registration.  s3r_host_stats: {frames delivered into a pinned buffer, frames copied into a
- * pageable one, successful registrations, registrations merged into a larger one, registrations
- * held, stale registrations replaced, frames delivered by host fill, fill threads}. */
+ * frame reaches it at the pinned rate.  A buffer sharing a page with an existing registration -- the
+ * second half of the reference's double buffer (one 2 * bufferSize allocation, main.swift:164)
+ * shares the seam page with the first -- is merged with it into one registration covering both.
+ * s3r_host_pinned: 1 if [ptr, ptr + bytes) lies inside a successful registration.  s3r_host_stats:
+ * {frames delivered into a pinned buffer, frames copied into a pageable one, successful
+ * registrations, registrations merged into a larger one, registrations held, stale registrations
+ * replaced, frames delivered by copy, by direct writes, by host fill, host fill threads, bytes the
+ * devices sent over their PCIe links for the last frame}. */
 int s3r_host_pinned(const void *ptr, uint64_t bytes);
-void s3r_host_stats(uint64_t out[8]);
+void s3r_host_stats(uint64_t out[11]);
 
-/* Host-fill delivery (default for the row path into a page-locked buffer): the GPU writes only the
- * frame's covered bins -- bins some triangle meets -- straight into the caller's buffer, and
- * `threads` library threads write the background of the sky bins meanwhile (render.cpp:282's fill),
- * so the PCIe link carries the covered bins only.  threads = 0: every pixel is rendered into device
- * memory and copied over the link; -1: S3R_FILL_THREADS or the default (8).  Pixels are identical
- * either way.  Returns 0, or -1 for threads > 64. */
-int s3r_set_fill_threads(int threads);
+/* How updateAndRender delivers the frame into a page-locked caller buffer (pixels identical in
+ * every mode):
+ *   1 copy    render into device memory, then a DMA copy over the PCIe link;
+ *   2 direct  the fragment kernel writes the pixels straight into the caller's buffer;
+ *   3 fill    host fill: the GPU writes only the bins some triangle meets, and `fill_threads`
+ *             library threads write the background of the others (render.cpp:282's fill)
+ *             meanwhile, so the link carries the covered bins only;
+ *   0 auto    (default) host fill on up to 2 devices, direct beyond; -1: S3R_DELIVERY
+ *             (copy|direct|fill|auto) or auto.
+ * Tile-path frames and buffers that cannot be page-locked are always copied.  fill_threads -1:
+ * S3R_FILL_THREADS or 8.  Returns 0, or -1 on a bad mode or thread count (0 or > 64).
+ * s3r_delivery() returns the mode in effect (0-3). */
+int s3r_set_delivery(int mode, int fill_threads);
+int s3r_delivery(void);
 
 /* Rows of a height-row frame owned by `part`. */
 uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);

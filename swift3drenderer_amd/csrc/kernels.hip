@@ -949,7 +949,10 @@ __device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMask
 // loads (79 VGPRs: occupancy 6).  It pays where the launch is throughput-bound (4K, 8K frames: +1.5 %,
 // +3.7 %); launches of one or two rounds of workgroups are bound by their heaviest bins' latency,
 // which the extra waterfall rounds lengthen (a 4K frame half: -4 %, 1080p: -4 %).
-template <uint32_t SEGCH, bool WF>
+// HOSTW: `out` is the whole frame in the caller's mapped host buffer (direct / host-fill delivery,
+// render_api.cpp): rows at their frame rows, stores crossing the PCIe link -- its own instance, so
+// profiles tell the delivered launches from the HBM ones.
+template <uint32_t SEGCH, bool WF, bool HOSTW>
 __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fragment(const TriSetup *__restrict__ tris, uint32_t nslots,
                                                   const float *__restrict__ rowtab, const uint32_t *__restrict__ tex,
                                                   uint32_t ntex, uint32_t *__restrict__ out, uint32_t W, uint32_t H,
@@ -958,7 +961,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   uint32_t *__restrict__ bincnt,
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order,
-                                                  uint32_t frame_rows, uint32_t host_fill) {
+                                                  uint32_t host_fill) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1011,8 +1014,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     }
     __syncthreads();
     const uint32_t npairs = sh.cnt;
-    // output row: local row lr of a compact part buffer, or (frame_rows) frame row y of a whole frame
-    const size_t orow = (size_t)(frame_rows ? y : lr) * W;
+    // output row: local row lr of a compact part buffer, or (HOSTW) frame row y of a whole frame
+    const size_t orow = (size_t)(HOSTW ? y : lr) * W;
     if (npairs == 0) {
         // no triangle meets this block (sky): background only (render.cpp:282), 16 B per lane where
         // the row segment is 16-B aligned -- unless the host fills sky bins (host_fill: the frame is
@@ -2072,16 +2075,20 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     }
     const char *wf_env = getenv("S3R_WATERFALL_BINS");                             // tuning / test override
     const uint64_t wf_bins = wf_env ? strtoull(wf_env, nullptr, 10) : S3R_WATERFALL_BINS;
-    auto kern = g_segch == 6 ? (blocks >= wf_bins ? k_fragment<6, true> : k_fragment<6, false>)
-              : g_segch == 3 ? k_fragment<3, false> : g_segch == 2 ? k_fragment<2, false> : k_fragment<1, false>;
+    auto pick = [&](auto hostw) {
+        constexpr bool HW = decltype(hostw)::value;
+        return g_segch == 6 ? (blocks >= wf_bins ? k_fragment<6, true, HW> : k_fragment<6, false, HW>)
+             : g_segch == 3 ? k_fragment<3, false, HW> : g_segch == 2 ? k_fragment<2, false, HW> : k_fragment<1, false, HW>;
+    };
+    auto kern = frame_rows ? pick(std::true_type{}) : pick(std::false_type{});
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, (uint32_t)frame_rows, (uint32_t)host_fill);
+                              done_flag, prev_tag, order, (uint32_t)host_fill);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           (uint32_t)frame_rows, (uint32_t)host_fill);
+                           (uint32_t)host_fill);
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in

@@ -293,11 +293,13 @@ struct Lib {
     uint64_t pinned_frames = 0, pageable_frames = 0, registrations = 0, merges = 0;
     uint64_t reg_epoch = 1;                    // bumped whenever a registration goes away
 
-    // host fill (updateAndRender, row path): the GPU writes covered bins straight into the caller's
-    // page-locked buffer, fill_threads library threads write the sky bins' background meanwhile
-    int fill_threads = -1;                     // -1: S3R_FILL_THREADS or the default; 0: off
+    // updateAndRender's delivery into the caller's buffer (see "deliveries" below): -1 unset (the
+    // S3R_DELIVERY environment or auto), 0 auto, 1 copy, 2 direct, 3 host fill
+    int delivery = -1;
+    int fill_threads = -1;                     // host fill threads; -1: S3R_FILL_THREADS or the default
     Pool fill_pool;
-    uint64_t host_fill_frames = 0;
+    uint64_t copy_frames = 0, direct_frames = 0, fill_frames = 0;
+    uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
 
 Lib g;
@@ -581,10 +583,11 @@ void release_all() {
     const int dev = g.device, rp = g.raster_path;
     const std::vector<int> ids = g.device_ids;
     const uint32_t band = g.band_rows;
-    const int fill = g.fill_threads;
+    const int fill = g.fill_threads, delivery = g.delivery;
     g.~Lib();
     new (&g) Lib();
     g.fill_threads = fill;
+    g.delivery = delivery;
     g.data_path = path;
     g.device = dev;
     g.raster_path = rp;
@@ -772,13 +775,15 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     HIPCHECK(hipGetLastError());
 }
 
-// Host fill for one frame part: the flags the sky-flag kernel writes (device address) and the tag.
+// A frame part written straight into the caller's mapped host buffer (direct / host-fill delivery):
+// with flags_dev (host fill) the sky-flag kernel publishes the bins' flags with this tag and the
+// fragment kernel leaves sky bins to the host; without, the fragment kernel writes every pixel.
 struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; };
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
 // band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
 // (row path only) `out` is the whole W x H frame in the caller's mapped host buffer: the fragment
-// kernel writes this part's covered bins at their frame rows and leaves the sky bins to the host.
+// kernel writes this part's bins at their frame rows -- only the covered ones for host fill.
 void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st, const HostFill *hf = nullptr) {
     TimingSlot *ts = timing_slot(d);
@@ -842,11 +847,11 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     d.hp.lap(2);
     const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, hf ? nullptr : d.geo_done[p],
-                    lpt ? d.order[p] : nullptr);
+                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo,
+                    hf && hf->flags_dev ? nullptr : d.geo_done[p], lpt ? d.order[p] : nullptr);
     // host fill: the bins' sky flags to the host as soon as the counts are final (before the
     // fragment kernel, which resets the counts, may start)
-    if (hf) launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, d.geo_done[p]);
+    if (hf && hf->flags_dev) launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, d.geo_done[p]);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
@@ -858,7 +863,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
-                    lpt ? d.order[p] : nullptr, hf != nullptr, hf != nullptr);
+                    lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -1018,22 +1023,44 @@ void deliver_part(void *arg, int i) {
     HIPCHECK(hipStreamSynchronize(d.stream));
 }
 
-// ---------------------------------------------------------------- host-fill delivery
-// updateAndRender's PCIe link carries every pixel of the frame in the copy delivery above, although
-// typically half the frame's bins are sky -- bins no triangle meets, all background (render.cpp:282).
-// Host fill: each device writes only its covered bins, straight into their rows of the caller's
-// mapped, page-locked buffer (k_fragment frame_rows + host_fill), and publishes every bin's sky flag
-// as soon as its geometry is done (k_sky_flags); meanwhile the library's fill threads write the sky
-// bins' background with streaming stores.  The link carries the covered bins only, and the host's
-// memory writes overlap the GPU's.
+// ---------------------------------------------------------------- deliveries
+// How updateAndRender's frame reaches the caller's host buffer.  The PCIe link is the bound: a 4K
+// frame is 33 MB, rendered in ~60 us but carried in ~0.6 ms.
+//   copy    every device renders its rows into HBM, then the DMA engine copies them into their rows
+//           of the caller's page-locked buffer (deliver_part above).
+//   direct  the fragment kernel writes its pixels straight into their rows of the caller's mapped,
+//           page-locked buffer (frame_rows): the link's transfer overlaps the rendering, and no DMA
+//           setup is paid (kernel stores to registered host memory measured at 55.7 GB/s against
+//           ~50 GB/s for the copy, tools/micro/pcie_write.hip).
+//   fill    (host fill) as direct, but typically half the frame's bins are sky -- bins no triangle
+//           meets, all background (render.cpp:282): each device publishes every bin's sky flag as
+//           soon as its geometry is done (k_sky_flags), writes only its covered bins, and the
+//           library's fill threads write the sky bins' background with streaming stores meanwhile.
+//           The link carries the covered bins only; the host's memory writes overlap the GPU's.
+// Auto: host fill for up to kFillMaxParts devices (one link carries the frame: halving its bytes
+// matters most), direct beyond (N links carry the frame, and host fill would put the sky bins of
+// every part on the host's memory bandwidth).  Tile-path frames and buffers that cannot be
+// page-locked are copied.
 constexpr int kDefaultFillThreads = 8;
+constexpr uint32_t kFillMaxParts = 2;
+enum Delivery_ { kAuto = 0, kCopy = 1, kDirect = 2, kFill = 3 };
+
+int delivery_mode() {
+    if (g.delivery < 0) {
+        const char *e = getenv("S3R_DELIVERY");
+        g.delivery = !e ? kAuto : !strcmp(e, "copy") ? kCopy : !strcmp(e, "direct") ? kDirect
+                   : !strcmp(e, "fill") ? kFill : kAuto;
+    }
+    return g.delivery;
+}
+
 constexpr uint32_t kFillBlock = 8;            // bins per fill-thread work block (contiguous: whole lines)
 
 int fill_threads() {
     if (g.fill_threads < 0) {
         const char *e = getenv("S3R_FILL_THREADS");
         const int v = e ? atoi(e) : kDefaultFillThreads;
-        g.fill_threads = v < 0 ? 0 : (v > 64 ? 64 : v);
+        g.fill_threads = v < 1 ? 1 : (v > 64 ? 64 : v);
     }
     return g.fill_threads;
 }
@@ -1051,18 +1078,23 @@ struct FillJob {
     FillPart parts[kMaxDevices];
     HostFill hf[kMaxDevices];
     std::atomic<bool> stale{false};  // pixel 0 checked before its bin was filled: the mapping is stale
+    std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
 };
 
-void fill_bin(const FillJob &job, const FillPart &fp, uint64_t b) {
+// Fills bin b's background; returns the pixels written.
+uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b) {
     const uint32_t blk = (uint32_t)(b / fp.segs), seg = (uint32_t)(b % fp.segs);
     const uint32_t xs = seg * fp.seg_px, xe = xs + fp.seg_px < job.W ? xs + fp.seg_px : job.W;
+    uint64_t px = 0;
     for (uint32_t k = 0; k < fp.rpb; k++) {
         const uint32_t lr = blk * fp.rpb + k;
         if (lr >= fp.rows_local) break;
         const uint32_t y = ((lr / fp.band) * fp.nparts + fp.part) * fp.band + lr % fp.band;
         if (y >= job.H) continue;
         s3r_host::fill_words(job.frame + (size_t)y * job.W + xs, xe - xs, kBackground);
+        px += xe - xs;
     }
+    return px;
 }
 
 // Fill thread idx (1..threads): the blocks of kFillBlock bins it owns in every part, each handled as
@@ -1078,6 +1110,7 @@ void fill_worker(void *arg, int idx) {
     size_t n = pend.size();
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t idle = 0;
+    uint64_t px = 0;
     while (n) {
         size_t keep = 0;
         for (size_t i = 0; i < n; i++) {
@@ -1090,7 +1123,7 @@ void fill_worker(void *arg, int idx) {
             // pixel 0's bin: the sky-flag kernel wrote kMapProbe there through its mapping first
             if ((e >> 48) == 0 && b == 0 && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
-            fill_bin(job, fp, b);
+            px += fill_bin(job, fp, b);
         }
         if (keep == n) {
             __builtin_ia32_pause();
@@ -1102,6 +1135,7 @@ void fill_worker(void *arg, int idx) {
         n = keep;
     }
     s3r_host::store_fence();
+    job.sky_px.fetch_add(px, std::memory_order_relaxed);
 }
 
 // The device address of host buffer p inside registration r on device d (cached per registration).
@@ -1121,7 +1155,7 @@ struct DirectDelivery {
     const Lib::Reg *reg;
 };
 
-// Part i of a host-fill frame on device i: render its covered bins into the caller's mapped buffer.
+// Part i of a direct / host-fill frame on device i: render it into the caller's mapped buffer.
 void deliver_part_direct(void *arg, int i) {
     const DirectDelivery &dd = *static_cast<const DirectDelivery *>(arg);
     FillJob &job = *dd.job;
@@ -1131,22 +1165,24 @@ void deliver_part_direct(void *arg, int i) {
     if (fp.rows_local && job.W) {
         uint32_t *frame_dev = mapped_ptr(d, *dd.reg, job.frame);
         HostFill hf = job.hf[i];
-        hf.probe_dev = i == 0 ? frame_dev : nullptr;
+        hf.probe_dev = i == 0 && hf.flags_dev ? frame_dev : nullptr;
         render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf);
     }
     HIPCHECK(hipStreamSynchronize(d.stream));
 }
 
-// One updateAndRender frame by host fill.  Returns false if the caller's registration turned out to
-// be stale (the frame did not reach the caller's pages: the caller redoes it by copy).
-bool host_fill_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts) {
+// One updateAndRender frame by direct delivery or host fill (fill).  Returns false if the caller's
+// registration turned out to be stale (the frame did not reach the caller's pages: the caller redoes
+// it by copy).
+bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, bool fill) {
     const Lib::Reg *reg = find_reg(buffer, (size_t)W * H * 4);
     FillJob job;
     job.frame = buffer;
     job.W = W;
     job.H = H;
     job.nparts = (int)nparts;
-    job.threads = fill_threads();
+    job.threads = fill ? fill_threads() : 0;
+    if (fill && g.fill_pool.workers() != job.threads) g.fill_pool.start(job.threads);
     const uint32_t band = nparts == 1 ? H : g.band;
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
@@ -1155,6 +1191,10 @@ bool host_fill_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts) 
         const FragLayout l = fragment_layout(W, fp.rows_local);
         fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
+        if (!fill) {
+            job.hf[i] = HostFill{nullptr, 0, nullptr};
+            continue;
+        }
         if (d.fill_cap < fp.bins) {
             HIPCHECK(hipSetDevice(d.device));
             if (d.fill_flags) HIPCHECK(hipHostFree(d.fill_flags));
@@ -1174,15 +1214,17 @@ bool host_fill_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts) 
         job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
-    buffer[0] = kStaleProbe;                          // k_sky_flags overwrites it via the mapping
+    buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
     DirectDelivery dd{&job, reg};
-    g.fill_pool.launch(fill_worker, &job, job.threads + 1);
+    if (fill) g.fill_pool.launch(fill_worker, &job, job.threads + 1);
     g.pool.run(deliver_part_direct, &dd, (int)nparts);
-    g.fill_pool.join();
-    // pixel 0 in a covered bin: the GPU wrote it (a pixel, neither probe) unless the mapping is stale
-    const uint32_t f0 = job.parts[0].bins ? job.parts[0].flags[0] : 0;
+    if (fill) g.fill_pool.join();
+    // pixel 0 written by the GPU (direct, or a covered bin under host fill) is a pixel, neither
+    // probe, unless the mapping is stale; under host fill a sky bin 0 was checked by its fill thread
+    const uint32_t f0 = fill && job.parts[0].bins ? job.parts[0].flags[0] : 0;
     const bool stale = job.stale.load() || (!(f0 & kSkyBit) && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
-    g.host_fill_frames++;
+    (fill ? g.fill_frames : g.direct_frames)++;
+    g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load());
     return !stale;
 }
 
@@ -1205,10 +1247,12 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     Delivery job{W, H, g.band, nparts, pixel_data->buffer, copy_bytes, false};
     bool pinned = false;
     if (copy_bytes) pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
-    if (pinned && npx && copy_bytes == frame_bytes && fill_threads() > 0 && !use_tile_path()) {
-        // host fill: covered bins by the GPU(s) straight into the buffer, sky bins by the host
-        if (g.fill_pool.workers() != g.fill_threads) g.fill_pool.start(g.fill_threads);
-        if (host_fill_frame(pixel_data->buffer, W, H, nparts)) {
+    const int mode = delivery_mode();
+    if (pinned && npx && copy_bytes == frame_bytes && mode != kCopy && !use_tile_path()) {
+        // direct / host fill: the GPU(s) write straight into the buffer (host fill: covered bins only,
+        // the sky bins by the host)
+        const bool fill = mode == kFill || (mode == kAuto && nparts <= kFillMaxParts);
+        if (mapped_frame(pixel_data->buffer, W, H, nparts, fill)) {
             g.pinned_frames++;
             for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
             HIPCHECK(hipSetDevice(g.devs[0]->device));
@@ -1222,8 +1266,10 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     if (copy_bytes) {
         if (pinned && copy_words) stamp_probes(pixel_data->buffer, copy_words);
         (pinned ? g.pinned_frames : g.pageable_frames)++;
+        g.copy_frames++;
     }
     if (npx) g.pool.run(deliver_part, &job, (int)nparts);
+    g.link_bytes = copy_bytes;
     for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
     if (pinned && copy_words && !probes_overwritten(pixel_data->buffer, copy_words)) {
         // a stale registration (buffer freed and reallocated at the same address): pin anew, copy again
@@ -1349,23 +1395,29 @@ __attribute__((visibility("default"))) int s3r_host_pinned(const void *ptr, uint
     return r && r->ok ? 1 : 0;
 }
 
-__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[8]) {
+__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[11]) {
     out[0] = g.pinned_frames;
     out[1] = g.pageable_frames;
     out[2] = g.registrations;
     out[3] = g.merges;
     out[4] = g.regs.size();
     out[5] = g.stale_pins;
-    out[6] = g.host_fill_frames;
-    out[7] = (uint64_t)fill_threads();
+    out[6] = g.copy_frames;
+    out[7] = g.direct_frames;
+    out[8] = g.fill_frames;
+    out[9] = (uint64_t)fill_threads();
+    out[10] = g.link_bytes;
 }
 
-__attribute__((visibility("default"))) int s3r_set_fill_threads(int threads) {
-    if (threads > 64) return -1;
+__attribute__((visibility("default"))) int s3r_set_delivery(int mode, int fill_threads) {
+    if (mode < -1 || mode > kFill || fill_threads == 0 || fill_threads > 64) return -1;
     g.fill_pool.stop();
-    g.fill_threads = threads < 0 ? -1 : threads;
+    g.delivery = mode;
+    g.fill_threads = fill_threads < 0 ? -1 : fill_threads;
     return 0;
 }
+
+__attribute__((visibility("default"))) int s3r_delivery(void) { return delivery_mode(); }
 
 __attribute__((visibility("default"))) void s3r_timing(int enable) {
     g.timing = enable != 0;

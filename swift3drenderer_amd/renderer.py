@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 EXPORTS = ['updateAndRender', 's3r_configure', 's3r_configure_devices', 's3r_devices', 's3r_shutdown',
            's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host', 's3r_host_pinned', 's3r_host_stats',
            's3r_render_bands', 's3r_bands_to_host', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect',
-           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_fill_threads']
+           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_delivery', 's3r_delivery']
 
 _lib = None
 # host frames of update_and_render(out=None), one per shape, kept for the process: the library may
@@ -68,8 +68,10 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_host_pinned.restype = ctypes.c_int
     lib.s3r_host_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_host_stats.restype = None
-    lib.s3r_set_fill_threads.argtypes = [ctypes.c_int]
-    lib.s3r_set_fill_threads.restype = ctypes.c_int
+    lib.s3r_set_delivery.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.s3r_set_delivery.restype = ctypes.c_int
+    lib.s3r_delivery.argtypes = []
+    lib.s3r_delivery.restype = ctypes.c_int
     missing = [name for name in EXPORTS if not hasattr(lib, name)]
     if missing:
         raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
@@ -114,17 +116,22 @@ class Renderer:
         return bool(self.lib.s3r_host_pinned(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
 
     def host_stats(self) -> dict:
-        out = (ctypes.c_uint64 * 8)()
+        out = (ctypes.c_uint64 * 11)()
         self.lib.s3r_host_stats(out)
-        keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale', 'host_fill_frames',
-                'fill_threads')
+        keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale', 'copy_frames',
+                'direct_frames', 'fill_frames', 'fill_threads', 'link_bytes')
         return dict(zip(keys, (int(v) for v in out)))
 
-    def set_fill_threads(self, threads: int):
-        """Host-fill delivery with `threads` fill threads (0: copy every pixel over the link; -1: the
-        S3R_FILL_THREADS / default)."""
-        if self.lib.s3r_set_fill_threads(int(threads)) != 0:
-            raise ValueError(f'bad fill thread count {threads}')
+    DELIVERIES = {'env': -1, 'auto': 0, 'copy': 1, 'direct': 2, 'fill': 3}
+
+    def set_delivery(self, mode='auto', fill_threads: int = -1):
+        """updateAndRender's delivery into the caller's buffer: 'auto', 'copy', 'direct', 'fill' (host
+        fill with `fill_threads` threads), or 'env' (S3R_DELIVERY); include/render.h."""
+        if self.lib.s3r_set_delivery(self.DELIVERIES.get(mode, mode), int(fill_threads)) != 0:
+            raise ValueError(f'bad delivery {mode!r} / {fill_threads}')
+
+    def delivery(self) -> str:
+        return {v: k for k, v in self.DELIVERIES.items()}[self.lib.s3r_delivery()]
 
     def update_and_render(self, width: int, height: int, inp, out: np.ndarray | None = None) -> np.ndarray:
         """updateAndRender into a host uint32 (H, W) buffer (the reference's contract).

@@ -163,22 +163,24 @@ def test_parts_pin_the_callers_double_buffer(multi, scene_dir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('fill', [0, 1, 3, 16])
+@pytest.mark.parametrize('mode,fill', [('copy', -1), ('direct', -1), ('fill', 1), ('fill', 3), ('fill', 16),
+                                       ('auto', -1)])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
-def test_delivery_modes_match_oracle(multi, scene_dir, fill, devices):
-    """Both deliveries of updateAndRender -- every pixel rendered into HBM and copied over the link
-    (fill 0), or covered bins written by the GPU straight into the caller's buffer while `fill` host
-    threads write the sky bins (render_api.cpp host fill) -- give the oracle's frames, on one device
-    and on three parts, at 4K (384-px bins) and 1080p (128-px bins)."""
+def test_delivery_modes_match_oracle(multi, scene_dir, mode, fill, devices):
+    """Every delivery of updateAndRender -- rendered into HBM and copied over the link, written by the
+    fragment kernel straight into the caller's buffer, or host fill (covered bins by the GPU, sky bins
+    by `fill` host threads; render_api.cpp) -- gives the oracle's frames, on one device and on three
+    parts, at 4K (384-px bins) and 1080p (128-px bins)."""
     try:
-        multi.set_fill_threads(fill)
+        multi.set_delivery(mode, fill)
         frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', 1920, 1080), devices)
         frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_id', 3840, 2160, extra=1), devices)
         st = multi.host_stats()                      # (counters restart at each configure)
-        assert st['fill_threads'] == fill
-        assert (st['host_fill_frames'] > 0) == (fill > 0), st
+        used = mode if mode != 'auto' else ('fill' if len(devices) <= 2 else 'direct')
+        assert st[f'{used}_frames'] == 2 and st['pinned_frames'] == 2, st
+        assert multi.delivery() == mode
     finally:
-        multi.set_fill_threads(-1)
+        multi.set_delivery('env')
 
 
 @pytest.mark.gpu
@@ -190,4 +192,4 @@ def test_host_fill_sparse_and_empty_frames(multi, scene_dir, tmp_path):
     frames_vs_oracle(multi, empty, pose_frames('P_over', 640, 480), [0])
     away = [(640, 480, (0, 0, 0, 0, 0, 0)), (640, 480, (0, 0, 0, 0, 4000.0, 0.0)), (640, 480, (0, 0, 0, 0, 8000.0, 0.0))]
     frames_vs_oracle(multi, scene_dir['full'], away, [0, 0])
-    assert multi.host_stats()['host_fill_frames'] > 0
+    assert multi.host_stats()['fill_frames'] > 0

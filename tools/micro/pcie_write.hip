@@ -108,7 +108,7 @@ int main() {
             Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<1, false>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
         report("kernel bins 4B/lane nontemporal", time_it(s, e0, e1, [](hipStream_t st, void *p) {
             Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<1, true>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
-        if (mode != 0) {   // 16-B stores need a 16-B aligned row segment
+        {   // (row segments are 16-B aligned in every mode)
             report("kernel bins 16B/lane", time_it(s, e0, e1, [](hipStream_t st, void *p) {
                 Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<4, false>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
             report("kernel bins 16B/lane nontemporal", time_it(s, e0, e1, [](hipStream_t st, void *p) {
