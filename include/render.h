@@ -131,7 +131,7 @@ void s3r_host_stats(uint64_t out[11]);
  *   0 auto    (default) host fill on up to 2 devices, direct beyond; -1: S3R_DELIVERY
  *             (copy|direct|fill|auto) or auto.
  * Tile-path frames and buffers that cannot be page-locked are always copied.  fill_threads -1:
- * S3R_FILL_THREADS or 8.  Returns 0, or -1 on a bad mode or thread count (0 or > 64).
+ * S3R_FILL_THREADS or 4.  Returns 0, or -1 on a bad mode or thread count (0 or > 64).
  * s3r_delivery() returns the mode in effect (0-3). */
 int s3r_set_delivery(int mode, int fill_threads);
 int s3r_delivery(void);

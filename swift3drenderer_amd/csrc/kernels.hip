@@ -304,6 +304,7 @@ constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + co
 #endif
 constexpr uint32_t kWaves = S3R_WAVES; // one wave per row: a workgroup is kWaves consecutive local rows
 static_assert(kWaves == 4, "pair records carry the walk state of 4 rows (s3r_kernels.h)");
+static_assert(kWaves * 6 <= 32, "host fill: a bin's chunk mask (rows x chunks) fits 32 bits");
 constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
 #ifndef S3R_STATE_BATCHES
 #define S3R_STATE_BATCHES 4
@@ -340,6 +341,7 @@ struct FragShared {
     float4 tab4[kWaves][kTables][kChunk / 4];  // exact S(c, d, k), k < kChunk, filled by sequential adds
     uint32_t cnt, next;
     uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
+    uint32_t bgm[kWaves];                // host fill: per wave (row), its chunks left to the host
 };
 static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
 // k_fragment stages a bin's pair records in tab4 before the chunk loop (s3r_kernels.h kPairMax x
@@ -961,7 +963,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   uint32_t *__restrict__ bincnt,
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order,
-                                                  uint32_t host_fill) {
+                                                  uint32_t host_fill, unsigned long long *chunk_flags,
+                                                  uint32_t fill_tag) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1094,6 +1097,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     }
 
     uint32_t *row = out + orow;
+    uint32_t bgm = 0;                    // host fill: this row's chunks no triangle covers (bit q)
     S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + kChunk * q;
@@ -1241,6 +1245,17 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         }
         S3R_WGC_ADD(1);
         S3R_WGC_MARK();
+        if (HOSTW && host_fill) {
+            // a chunk of this row without a winner is all background: the host writes it (bit q of
+            // this bin's chunk flag), so the link does not carry it
+            bool any = false;
+#pragma unroll
+            for (uint32_t p = 0; p < kPX; p++) any |= row_ok && x + 64u * p <= xe && win[p] >= 0;
+            if (__ballot(any) == 0) {
+                if (row_ok) bgm |= 1u << q;
+                continue;
+            }
+        }
 #pragma unroll
         for (uint32_t p = 0; p < kPX; p++) {
             const uint32_t xp = x + 64u * p;
@@ -1288,6 +1303,18 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 #endif
         }
         S3R_WGC_ADD(2);
+    }
+    if (HOSTW && host_fill) {
+        // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q)
+        if (lane == 0) sh.bgm[wave] = bgm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kWaves; w++) m |= sh.bgm[w] << (w * SEGCH);
+            __hip_atomic_store(chunk_flags + bid, ((unsigned long long)fill_tag << 32) | m, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     S3R_WGT(3);
     // this bin's cost (wave 0's wall time, 10 ns ticks) for the buffer set's next order_bins
@@ -2032,6 +2059,7 @@ FragLayout fragment_layout(uint32_t W, uint32_t rows_local) {
     l.seg_px = kChunk * segment_chunks(W, rows_local);
     l.segs = (W + l.seg_px - 1) / l.seg_px;
     l.rows_per_bin = kWaves;
+    l.chunk_px = kChunk;
     l.bins = (uint64_t)((rows_local + kWaves - 1) / kWaves) * l.segs;
     return l;
 }
@@ -2066,7 +2094,7 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
-                     bool frame_rows, bool host_fill) {
+                     bool frame_rows, bool host_fill, unsigned long long *chunk_flags, uint32_t fill_tag) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2084,11 +2112,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, (uint32_t)host_fill);
+                              done_flag, prev_tag, order, (uint32_t)host_fill, chunk_flags, fill_tag);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           (uint32_t)host_fill);
+                           (uint32_t)host_fill, chunk_flags, fill_tag);
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in

@@ -144,6 +144,7 @@ struct Dev {
     // host fill: one flag per fragment bin (host-coherent; k_sky_flags), this device's tag sequence,
     // and the device address of the caller-buffer registration the last host-fill frame used
     uint32_t *fill_flags = nullptr, *fill_flags_dev = nullptr;
+    unsigned long long *fill_chunks = nullptr, *fill_chunks_dev = nullptr;   // per bin: (tag << 32) | chunk mask
     uint64_t fill_cap = 0;
     uint32_t fill_tag = 0;
     uintptr_t map_host = 0, map_dev = 0;
@@ -550,6 +551,7 @@ void dev_release(Dev &d) {
     if (d.handoff) (void)hipEventDestroy(d.handoff);
     if (d.tile_total_host) (void)hipHostFree(d.tile_total_host);
     if (d.fill_flags) (void)hipHostFree(d.fill_flags);
+    if (d.fill_chunks) (void)hipHostFree(d.fill_chunks);
     for (int p = 0; p < kSets; p++) {
         if (d.geo_done[p]) (void)hipEventDestroy(d.geo_done[p]);
         if (d.frag_done[p]) (void)hipEventDestroy(d.frag_done[p]);
@@ -776,9 +778,10 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
 }
 
 // A frame part written straight into the caller's mapped host buffer (direct / host-fill delivery):
-// with flags_dev (host fill) the sky-flag kernel publishes the bins' flags with this tag and the
-// fragment kernel leaves sky bins to the host; without, the fragment kernel writes every pixel.
-struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; };
+// with flags_dev (host fill) the sky-flag kernel publishes the bins' flags with this tag, and the
+// fragment kernel leaves sky bins and, in covered bins, the row chunks without a winner to the host
+// (their masks in chunks_dev); without, the fragment kernel writes every pixel.
+struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; unsigned long long *chunks_dev; };
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
 // band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
@@ -863,7 +866,8 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
-                    lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev);
+                    lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev, hf ? hf->chunks_dev : nullptr,
+                    hf ? hf->tag : 0u);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -1041,7 +1045,7 @@ void deliver_part(void *arg, int i) {
 // matters most), direct beyond (N links carry the frame, and host fill would put the sky bins of
 // every part on the host's memory bandwidth).  Tile-path frames and buffers that cannot be
 // page-locked are copied.
-constexpr int kDefaultFillThreads = 8;
+constexpr int kDefaultFillThreads = 4;     // measured: 2 CPU-bound, 8-16 add scheduling jitter (p90)
 constexpr uint32_t kFillMaxParts = 2;
 enum Delivery_ { kAuto = 0, kCopy = 1, kDirect = 2, kFill = 3 };
 
@@ -1066,8 +1070,9 @@ int fill_threads() {
 }
 
 struct FillPart {
-    uint32_t *flags;                 // host view of the device's flags
-    uint32_t tag, seg_px, segs, rpb, rows_local, band, nparts, part;
+    uint32_t *flags;                 // host view of the device's sky flags
+    unsigned long long *chunks;      // host view of its covered bins' chunk masks
+    uint32_t tag, seg_px, segs, rpb, chunk_px, rows_local, band, nparts, part;
     uint64_t bins;
 };
 
@@ -1081,24 +1086,41 @@ struct FillJob {
     std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
 };
 
-// Fills bin b's background; returns the pixels written.
-uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b) {
+// Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
+// row_in_bin * chunks_per_row + chunk) of a covered bin; returns the pixels written.
+uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, uint32_t mask) {
     const uint32_t blk = (uint32_t)(b / fp.segs), seg = (uint32_t)(b % fp.segs);
     const uint32_t xs = seg * fp.seg_px, xe = xs + fp.seg_px < job.W ? xs + fp.seg_px : job.W;
+    const uint32_t cpr = fp.seg_px / fp.chunk_px;
     uint64_t px = 0;
     for (uint32_t k = 0; k < fp.rpb; k++) {
         const uint32_t lr = blk * fp.rpb + k;
         if (lr >= fp.rows_local) break;
         const uint32_t y = ((lr / fp.band) * fp.nparts + fp.part) * fp.band + lr % fp.band;
         if (y >= job.H) continue;
-        s3r_host::fill_words(job.frame + (size_t)y * job.W + xs, xe - xs, kBackground);
-        px += xe - xs;
+        uint32_t *row = job.frame + (size_t)y * job.W;
+        if (sky) {
+            s3r_host::fill_words(row + xs, xe - xs, kBackground);
+            px += xe - xs;
+            continue;
+        }
+        for (uint32_t q = 0; q < cpr; q++) {
+            if (!((mask >> (k * cpr + q)) & 1u)) continue;
+            const uint32_t c0 = xs + q * fp.chunk_px, c1 = c0 + fp.chunk_px < xe ? c0 + fp.chunk_px : xe;
+            if (c0 >= c1) continue;
+            s3r_host::fill_words(row + c0, c1 - c0, kBackground);
+            px += c1 - c0;
+        }
     }
     return px;
 }
 
 // Fill thread idx (1..threads): the blocks of kFillBlock bins it owns in every part, each handled as
-// soon as its flags carry this frame's tag -- sky bins filled, covered ones left to the GPU.
+// soon as its flags carry this frame's tag: a sky bin (k_sky_flags, right after the geometry) is
+// filled whole; a covered bin waits for its workgroup's chunk mask (end of the workgroup) and gets
+// the row chunks without a winner filled.
+constexpr uint64_t kWaitChunks = 1ull << 47;    // pending entry: sky flag seen, covered, mask awaited
+
 void fill_worker(void *arg, int idx) {
     FillJob &job = *static_cast<FillJob *>(arg);
     const uint64_t t = (uint64_t)idx - 1, T = (uint64_t)job.threads;
@@ -1115,15 +1137,27 @@ void fill_worker(void *arg, int idx) {
         size_t keep = 0;
         for (size_t i = 0; i < n; i++) {
             const uint64_t e = pend[i];
-            const FillPart &fp = job.parts[e >> 48];
-            const uint64_t b = e & 0xFFFFFFFFFFFFull;
-            const uint32_t f = __atomic_load_n(fp.flags + b, __ATOMIC_ACQUIRE);
-            if ((f & ~kSkyBit) != fp.tag) { pend[keep++] = e; continue; }
-            if (!(f & kSkyBit)) continue;
-            // pixel 0's bin: the sky-flag kernel wrote kMapProbe there through its mapping first
-            if ((e >> 48) == 0 && b == 0 && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
+            const uint32_t part = (uint32_t)(e >> 48);
+            const FillPart &fp = job.parts[part];
+            const uint64_t b = e & (kWaitChunks - 1);
+            bool sky = false;
+            uint32_t mask = 0;
+            if (!(e & kWaitChunks)) {
+                const uint32_t f = __atomic_load_n(fp.flags + b, __ATOMIC_ACQUIRE);
+                if ((f & ~kSkyBit) != fp.tag) { pend[keep++] = e; continue; }
+                if (!(f & kSkyBit)) { pend[keep++] = e | kWaitChunks; continue; }
+                sky = true;
+            } else {
+                const unsigned long long c = __atomic_load_n(fp.chunks + b, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(c >> 32) != fp.tag) { pend[keep++] = e; continue; }
+                mask = (uint32_t)c;
+                if (!mask) continue;
+            }
+            // pixel 0 (part 0, bin 0, its first row and chunk): the sky-flag kernel wrote kMapProbe
+            // there through its mapping before publishing the bin's flag
+            if (part == 0 && b == 0 && (sky || (mask & 1u)) && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
-            px += fill_bin(job, fp, b);
+            px += fill_bin(job, fp, b, sky, mask);
         }
         if (keep == n) {
             __builtin_ia32_pause();
@@ -1189,29 +1223,36 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
         FillPart &fp = job.parts[i];
         fp.rows_local = nparts == 1 ? H : band_rows_local(H, band, nparts, i);
         const FragLayout l = fragment_layout(W, fp.rows_local);
-        fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.bins = fp.rows_local ? l.bins : 0;
+        fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.chunk_px = l.chunk_px;
+        fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
         if (!fill) {
-            job.hf[i] = HostFill{nullptr, 0, nullptr};
+            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr};
             continue;
         }
         if (d.fill_cap < fp.bins) {
             HIPCHECK(hipSetDevice(d.device));
             if (d.fill_flags) HIPCHECK(hipHostFree(d.fill_flags));
-            HIPCHECK(hipHostMalloc((void **)&d.fill_flags, fp.bins * sizeof(uint32_t),
-                                   hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+            if (d.fill_chunks) HIPCHECK(hipHostFree(d.fill_chunks));
+            const unsigned flags = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+            HIPCHECK(hipHostMalloc((void **)&d.fill_flags, fp.bins * sizeof(uint32_t), flags));
+            HIPCHECK(hipHostMalloc((void **)&d.fill_chunks, fp.bins * sizeof(unsigned long long), flags));
             memset(d.fill_flags, 0, fp.bins * sizeof(uint32_t));
+            memset(d.fill_chunks, 0, fp.bins * sizeof(unsigned long long));
             HIPCHECK(hipHostGetDevicePointer((void **)&d.fill_flags_dev, d.fill_flags, 0));
+            HIPCHECK(hipHostGetDevicePointer((void **)&d.fill_chunks_dev, d.fill_chunks, 0));
             d.fill_cap = fp.bins;
             d.fill_tag = 0;
         }
         if (++d.fill_tag >= kSkyBit) {                 // (after 2^31 frames) restart the tags
             memset(d.fill_flags, 0, d.fill_cap * sizeof(uint32_t));
+            memset(d.fill_chunks, 0, d.fill_cap * sizeof(unsigned long long));
             d.fill_tag = 1;
         }
         fp.flags = d.fill_flags;
+        fp.chunks = d.fill_chunks;
         fp.tag = d.fill_tag;
-        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr};
+        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
@@ -1219,10 +1260,13 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
     if (fill) g.fill_pool.launch(fill_worker, &job, job.threads + 1);
     g.pool.run(deliver_part_direct, &dd, (int)nparts);
     if (fill) g.fill_pool.join();
-    // pixel 0 written by the GPU (direct, or a covered bin under host fill) is a pixel, neither
-    // probe, unless the mapping is stale; under host fill a sky bin 0 was checked by its fill thread
-    const uint32_t f0 = fill && job.parts[0].bins ? job.parts[0].flags[0] : 0;
-    const bool stale = job.stale.load() || (!(f0 & kSkyBit) && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
+    // pixel 0 written by the GPU (direct, or a covered chunk under host fill) is a pixel, neither
+    // probe, unless the mapping is stale; a pixel 0 the host filled was checked by its fill thread
+    bool host0 = false;
+    if (fill && job.parts[0].bins) {
+        host0 = (job.parts[0].flags[0] & kSkyBit) || (job.parts[0].chunks[0] & 1ull);
+    }
+    const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
     (fill ? g.fill_frames : g.direct_frames)++;
     g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load());
     return !stale;

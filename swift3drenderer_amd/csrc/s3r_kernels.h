@@ -13,12 +13,15 @@ namespace s3r {
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact,
 // out[lr * W + x], or with frame_rows the whole frame's row, out[y * W + x] (out = a W x H frame, e.g.
 // the caller's host buffer).  host_fill: sky bins (no triangle) write nothing -- the host fills them
-// (launch_sky_flags).
+// (launch_sky_flags) -- and neither do the row chunks of covered bins that end without a winner:
+// each bin's workgroup stores chunk_flags[bin] = (fill_tag << 32) | mask at its end, bit
+// (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
-                     bool frame_rows = false, bool host_fill = false);
+                     bool frame_rows = false, bool host_fill = false, unsigned long long *chunk_flags = nullptr,
+                     uint32_t fill_tag = 0);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
 // pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0
@@ -48,7 +51,7 @@ uint32_t fragment_segment_pixels();
 // The row path's fragment bins for a frame part of W x rows_local (what fragment_configure picks):
 // bin b covers local rows (b / segs) * rows_per_bin ... + rows_per_bin - 1, columns
 // (b % segs) * seg_px ... + seg_px - 1 (clipped to the part and the frame).
-struct FragLayout { uint32_t seg_px, segs, rows_per_bin; uint64_t bins; };
+struct FragLayout { uint32_t seg_px, segs, rows_per_bin, chunk_px; uint64_t bins; };
 FragLayout fragment_layout(uint32_t W, uint32_t rows_local);
 
 // Host fill: flags[b] = tag | (kSkyBit if bin b has no pair) for the bins' counts of the geometry
