@@ -33,6 +33,9 @@
  */
 #define _GNU_SOURCE
 #include <math.h>
+#if ORACLE_RSQRT
+#include <immintrin.h>
+#endif
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -59,7 +62,22 @@ static inline float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.
 static inline f3 cross3(f3 a, f3 b) {
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-static inline f3 fast_normalize3(f3 a) { return muls3(a, 1.0f / sqrtf(dot3(a, a))); }
+/* Sensitivity variants (tools/parity_sensitivity.py; never the parity oracle): ORACLE_RSQRT = 1
+ * takes simd_fast_normalize's 1/sqrt from the hardware estimate (x86 rsqrtss, relative error
+ * <= 1.5 * 2^-12), 2 adds one Newton-Raphson step -- the kind of approximation Apple's "fast"
+ * variant is allowed to make (render.cpp:142-147, :367-369). */
+static inline float inv_sqrt(float x) {
+#if ORACLE_RSQRT
+    float y = _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x)));
+#if ORACLE_RSQRT == 2
+    y = y * (1.5f - 0.5f * x * y * y);
+#endif
+    return y;
+#else
+    return 1.0f / sqrtf(x);
+#endif
+}
+static inline f3 fast_normalize3(f3 a) { return muls3(a, inv_sqrt(dot3(a, a))); }
 static inline f3 max3(f3 a, f3 b) { return v3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
 static inline f3 min3(f3 a, f3 b) { return v3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
 static inline f2 v2(float x, float y) { f2 r = {x, y}; return r; }
@@ -128,7 +146,12 @@ static void reset_state(void) {
     cfg_factor = 1;
     {
         const float fov = (float)M_PI / 5.f;
+#if ORACLE_TAN_DOUBLE
+        /* sensitivity variant: near * tan evaluated in double, then rounded to float */
+        cfg_scale = (float)((double)cfg_near * tan((double)(fov / 2)));
+#else
         cfg_scale = cfg_near * tanf(fov / 2);                             /* :92 */
+#endif
     }
 }
 
@@ -482,6 +505,7 @@ int oracle_set_row_windows(const uint32_t *rows, uint32_t n) {
 /* Debug view of the camera matrix (rows), for host-logic tests. */
 void oracle_camera_matrix(float out[12]) { memcpy(out, state.m, sizeof state.m); }
 float oracle_factor(void) { return cfg_factor; }
+float oracle_scale(void) { if (cfg_scale == 0) reset_state(); return cfg_scale; }
 
 /* Exact sequential float32 walk: s_{k+1} = fl(s_k + d), n times (render.cpp:374-379). */
 float oracle_repeat_add(float s, float d, uint32_t n) {

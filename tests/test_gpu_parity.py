@@ -279,3 +279,14 @@ def test_widest_segments_match_oracle(gpu_renderer, scene_dir, monkeypatch, scen
     want = oracle_render_pose(path, script, w, h, extra_frames=1)
     got = render_pose(gpu_renderer, path, script, w, h, extra_frames=1)
     assert np.array_equal(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize('height', [240, 480, 1080, 2160, 4320])
+def test_factor_known_answer_gpu(gpu_renderer, scene_dir, height):
+    """The library's raster factor (render.cpp:279, host float32) has the correctly rounded bits
+    pinned in tests/test_oracle.py."""
+    from test_oracle import FACTOR_BITS, f32_bits
+    gpu_renderer.configure(scene_dir['tetra'])
+    gpu_renderer.update_and_render(8, height, (0, 0, 0, 0, 0, 0))
+    _, factor = gpu_renderer.camera()
+    assert f32_bits(factor) == FACTOR_BITS[height]

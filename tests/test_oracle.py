@@ -114,3 +114,46 @@ def test_row_windows_equal_full_frame_rows(scene_dir, scene_name, pose):
     assert np.array_equal(out[mask], full[mask])
     assert (out[~mask] == 0x1E1E1E).all()
     assert (full[mask] != 0x1E1E1E).any()
+
+
+# config.scale = near * tan(fov / 2) with fov = (float)M_PI / 5 (render.cpp:89-92) and
+# factor = near * height / (2 * scale) (render.cpp:279), pinned to the correctly rounded float32
+# values: tan(fov / 2) lies 0.18 ulp from its float, far from a rounding tie, so every faithful tanf
+# (glibc's, Apple's) and a double-precision tan rounded to float give these same bits.
+SCALE_BITS = 0x3D05164D
+FACTOR_BITS = {240: 0x43B8A938, 480: 0x4438A938, 1080: 0x44CFBE5F, 2160: 0x454FBE5F, 4320: 0x45CFBE5F}
+
+
+def f32_bits(x) -> int:
+    return int(np.float32(x).view(np.uint32))
+
+
+def test_config_scale_known_answer():
+    import math
+    f32 = np.float32
+    half = f32(f32(math.pi) / f32(5)) / f32(2)
+    tan_f = f32(math.tan(float(half)))
+    assert f32_bits(f32(0.1) * tan_f) == SCALE_BITS
+    r = OracleRenderer.__new__(OracleRenderer)
+    r._l = None
+    assert f32_bits(r.scale()) == SCALE_BITS
+
+
+@pytest.mark.parametrize('height', sorted(FACTOR_BITS))
+def test_factor_known_answer(scene_dir, height):
+    r = OracleRenderer(scene_dir['tetra'])
+    r.update_and_render(8, height, (0, 0, 0, 0, 0, 0))
+    assert f32_bits(r.factor()) == FACTOR_BITS[height]
+
+
+def test_parity_sensitivity_tool_runs():
+    """tools/parity_sensitivity.py: the variants build and load, and the one that
+    cannot move pixels (double-precision tan, same float bits) moves none."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, 'tools', 'parity_sensitivity.py'), '--cases', '1'],
+                       capture_output=True, text=True, timeout=300, check=True)
+    summary = json.loads(r.stdout.strip().splitlines()[-1])['summary']
+    assert summary['tan_double']['differ'] == 0
+    assert summary['rsqrt12']['differ'] > 0          # the approximate rsqrt does move pixels
