@@ -20,6 +20,7 @@
 #include "s3r_kernels.h"
 
 #include <hip/hip_ext.h>
+#include <rocprim/device/device_scan.hpp>
 
 namespace s3r {
 
@@ -1339,7 +1340,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 //   k_tile_setup   one thread per triangle, POSITIONS ONLY (vertex transform, reject, near clip,
 //                  cull, raster setup; render.cpp:285-336): a 64-B RasterRec per live slot, a packed
 //                  bbox word per triangle, and the per-tile counts (wave-aggregated atomics);
-//   k_tile_scan    exclusive scan of the counts;   k_tile_fill  scatter slot ids into tile lists;
+//   (scan)         rocprim exclusive scan of the (tile, depth bucket) counts; k_tile_fill scatters slot
+//                  ids into the tile lists, each tile's depth buckets nearest first;
 //   k_tile_raster  one workgroup per tile of 16 local rows x 64 px: lanes take (triangle, row)
 //                  items and walk the row with the reference's own sequential adds (render.cpp:374,
 //                  :378; row start by exact_walk), keeping per pixel the max of
@@ -1356,6 +1358,25 @@ constexpr uint32_t kTileW = 64, kTileH = 16, kTileThreads = 256, kTileStage = S3
 static_assert(kTileStage <= kTileThreads, "one staged triangle per thread at most");
 constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of one column hit different banks
 constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
+
+// Depth buckets of a tile's list (nearest first).  A listed triangle's bucket is the half-octave of
+// its 1/z bound (ooz_bound) below 1/near = 10, the largest 1/z any pixel can have: bucket
+// b = (bits(10) >> 22) - (bits(bound) >> 22), clamped to [0, kDepthBuckets): 16 octaves, z up to
+// ~6 500.  Every bound in bucket b >= 1 is below bucket_ceiling(b); k_tile_raster walks a tile's
+// buckets in order and stops as soon as every pixel of the tile holds a winner at least that near.
+#ifndef S3R_DEPTH_BUCKETS
+#define S3R_DEPTH_BUCKETS 32
+#endif
+constexpr uint32_t kDepthBuckets = S3R_DEPTH_BUCKETS;
+constexpr uint32_t kBucketTop = 0x41200000u >> 22;  // bits(10.0f) >> 22
+__device__ __forceinline__ uint32_t depth_bucket(uint32_t zb_bits) {
+    const int b = (int)kBucketTop - (int)(zb_bits >> 22);
+    return (uint32_t)min(max(b, 0), (int)kDepthBuckets - 1);
+}
+// bits of an upper bound (exclusive) of every bound in bucket b (b = 0: none)
+__device__ __forceinline__ uint32_t bucket_ceiling(uint32_t b) {
+    return b == 0 ? 0xFFFFFFFFu : (kBucketTop - b + 1u) << 22;
+}
 
 struct alignas(16) RasterRec {                     // 64 B: one line per live slot
     uint32_t bx, by, slot, zb;                     // bx = xmin | xmax << 16, by = ymin | ymax << 16,
@@ -1412,18 +1433,26 @@ __device__ __forceinline__ bool local_row_range(uint32_t ymin, uint32_t ymax, ui
     return true;
 }
 
-struct TileSpan { uint32_t tx0, ntx, ty0, n; };     // tiles tx0 .. tx0+ntx-1 x ty0 .., n in all
+struct TileSpan { uint32_t tx0, ntx, ty0, n, bucket; };   // tiles tx0 .. tx0+ntx-1 x ty0 .., n in all
 
-__device__ __forceinline__ TileSpan box_tiles(uint32_t bx, uint32_t by, uint32_t band, uint32_t nparts, uint32_t part) {
-    TileSpan sp{0, 1, 0, 0};
+// The tiles of a box given in tile columns: bt = tx0 | tx1 << 12 | bucket << 24 (kDeadBox: none),
+// by = ymin | ymax << 16 in frame rows.
+__device__ __forceinline__ TileSpan box_tiles(uint32_t bt, uint32_t by, uint32_t band, uint32_t nparts, uint32_t part) {
+    TileSpan sp{0, 1, 0, 0, 0};
     uint32_t lo, hi;
-    if (bx == kDeadBox || !local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi)) return sp;
-    sp.tx0 = (bx & 0xFFFFu) / kTileW;
-    sp.ntx = (bx >> 16) / kTileW - sp.tx0 + 1u;
+    if (bt == kDeadBox || !local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi)) return sp;
+    sp.tx0 = bt & 0xFFFu;
+    sp.ntx = ((bt >> 12) & 0xFFFu) - sp.tx0 + 1u;
     sp.ty0 = lo / kTileH;
     sp.n = sp.ntx * (hi / kTileH - sp.ty0 + 1u);
+    sp.bucket = bt >> 24;
     return sp;
 }
+// The packed tile box of a raster record's pixel bbox bx = xmin | xmax << 16 and bound bits zb.
+__device__ __forceinline__ uint32_t tile_box(uint32_t bx, uint32_t zb) {
+    return ((bx & 0xFFFFu) / kTileW) | (((bx >> 16) / kTileW) << 12) | (depth_bucket(zb) << 24);
+}
+static_assert(kDepthBuckets <= 64, "bucket field of a packed tile box");
 
 // Every lane adds 1 to counter[key] for each tile of its span (or nothing); lanes of the wave with
 // the same key share one atomic.  With `list`, the returned positions place `slot` in the lists.
@@ -1441,7 +1470,8 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
         for (uint32_t q = 0; q < kSteps; q++) {
             const uint32_t k = k0 + q;
             const bool act = k < sp.n;
-            key[q] = act ? (sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx : 0xFFFFFFFFu;
+            key[q] = act ? ((sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx) * kDepthBuckets + sp.bucket
+                         : 0xFFFFFFFFu;
             uint64_t todo = __ballot(act);
             uint32_t my_leader = 0, my_rank = 0, cnt = 0;
             while (todo) {
@@ -1504,10 +1534,9 @@ __device__ float ooz_bound(const TriSetup &t) {
     return is_finite(up) && rmax > 0.0 && asum > 0.0 ? up : __builtin_inff();
 }
 
-__device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot) {
+__device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot, uint32_t zb) {
     float4 *q = reinterpret_cast<float4 *>(r);
-    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot,
-                                                 f2u(ooz_bound(t)));
+    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot, zb);
     q[1] = make_float4(t.ws[0], t.ws[1], t.ws[2], t.dx[0]);
     q[2] = make_float4(t.dx[1], t.dx[2], t.dy[0], t.dy[1]);
     q[3] = make_float4(t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]);
@@ -1540,14 +1569,16 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
                 if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) {
                     TriSetup ta;
                     if (raster_part(app, sw, sh, ta)) {
-                        const TileSpan sa = box_tiles(ta.xmin | (ta.xmax << 16), ta.ymin | (ta.ymax << 16), band,
-                                                      nparts, part);
+                        const uint32_t zba = f2u(ooz_bound(ta));
+                        const TileSpan sa = box_tiles(tile_box(ta.xmin | (ta.xmax << 16), zba), ta.ymin | (ta.ymax << 16),
+                                                      band, nparts, part);
                         if (sa.n) {                     // only triangles meeting this part's rows
-                            write_rec(recs + ntri + t, ta, ntri + t);
+                            write_rec(recs + ntri + t, ta, ntri + t, zba);
                             app_list[atomicAdd(app_count, 1u)] = ntri + t;
                         }
                         for (uint32_t k = 0; k < sa.n; k++)
-                            atomicAdd(&counts[(sa.ty0 + k / sa.ntx) * tiles_x + sa.tx0 + k % sa.ntx], 1u);
+                            atomicAdd(&counts[((sa.ty0 + k / sa.ntx) * tiles_x + sa.tx0 + k % sa.ntx) * kDepthBuckets +
+                                              sa.bucket], 1u);
                     }
                 }
             }
@@ -1555,14 +1586,16 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
         }
     }
     uint32_t bx = kDeadBox, by = 0;
-    TileSpan sp{0, 1, 0, 0};
+    TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
-        sp = box_tiles(ts.xmin | (ts.xmax << 16), ts.ymin | (ts.ymax << 16), band, nparts, part);
+        const uint32_t zb = f2u(ooz_bound(ts));
+        const uint32_t bt = tile_box(ts.xmin | (ts.xmax << 16), zb);
+        sp = box_tiles(bt, ts.ymin | (ts.ymax << 16), band, nparts, part);
         // a triangle outside this part's rows (row-band split) is dead here: no record, no box
         if (sp.n) {
-            bx = ts.xmin | (ts.xmax << 16);
+            bx = bt;
             by = ts.ymin | (ts.ymax << 16);
-            write_rec(recs + t, ts, t);
+            write_rec(recs + t, ts, t, zb);
         }
     }
     if (in) reinterpret_cast<uint2 *>(boxes)[t] = make_uint2(bx, by);
@@ -1572,26 +1605,14 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     tile_visit(sp, tiles_x, counts, nullptr, 0);
 }
 
-// Exclusive scan of the tile counts (one workgroup): offs[t], cursor[t] = offs[t], *total.
-__global__ void __launch_bounds__(1024) k_tile_scan(const uint32_t *__restrict__ counts, uint32_t ntiles,
-                                                    uint32_t *__restrict__ offs, uint32_t *__restrict__ cursor,
-                                                    uint32_t *__restrict__ total) {
-    __shared__ uint32_t part_sum[1024];
-    const uint32_t per = (ntiles + 1023u) / 1024u;
-    const uint32_t b = threadIdx.x * per, e = min(ntiles, b + per);
-    uint32_t sum = 0;
-    for (uint32_t i = b; i < e; i++) sum += counts[i];
-    part_sum[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024u; o <<= 1) {          // Hillis-Steele inclusive scan
-        const uint32_t v = threadIdx.x >= o ? part_sum[threadIdx.x - o] : 0u;
-        __syncthreads();
-        part_sum[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = part_sum[threadIdx.x] - sum;
-    for (uint32_t i = b; i < e; i++) { offs[i] = run; cursor[i] = run; run += counts[i]; }
-    if (threadIdx.x == 1023u) *total = part_sum[1023];
+// After the exclusive scan of the (tile, bucket) counts (rocprim, launch_tile_setup): the fill's
+// scatter cursors start at the offsets, and *total = the list length.
+__global__ void __launch_bounds__(256) k_tile_cursor(const uint32_t *__restrict__ counts, const uint32_t *__restrict__ offs,
+                                                     uint32_t n, uint32_t *__restrict__ cursor, uint32_t *__restrict__ total) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    cursor[i] = offs[i];
+    if (i == n - 1u) *total = offs[i] + counts[i];
 }
 
 // Scatter: threads [0, ntri) the original triangles (packed bboxes), then the clip-appended slots.
@@ -1608,7 +1629,7 @@ __global__ void __launch_bounds__(256) k_tile_fill(const uint32_t *__restrict__ 
     } else if (i - ntri < napp) {
         slot = app_list[i - ntri];
         const uint4 h = reinterpret_cast<const uint4 *>(recs + slot)[0];
-        bx = h.x; by = h.y;
+        bx = tile_box(h.x, h.w); by = h.y;
     }
     tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, slot);
 }
@@ -1620,6 +1641,8 @@ struct TileShared {
     uint32_t pre[kTileStage + 1];
     uint16_t item[kTileStage * kTileH];            // item -> staged triangle
     uint32_t wsum[kTileThreads / 64];
+    uint32_t bstart[kDepthBuckets];                // the tile's list position where each depth bucket starts
+    uint32_t zwave[kTileThreads / 64];             // per wave: min over its pixels of the winner's 1/z bits
     uint32_t zmin[kTileH][kTileW / 16];            // per tile row and 16-px group: min over its pixels of
                                                    // bits(1/z) of the current winner (0: a pixel has none)
 };
@@ -1665,7 +1688,10 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
     auto row_of = [&](uint32_t lr) { return nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band; };
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
-    const uint32_t n = counts[tile], base = offs[tile];
+    // the tile's list: its depth buckets, nearest first, one after another
+    const uint32_t s0 = tile * kDepthBuckets, sl = s0 + kDepthBuckets - 1u;
+    const uint32_t base = offs[s0], n = offs[sl] + counts[sl] - base;
+    if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
     // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
     // while stage c0's items run
     uint32_t s_nx = 0;
@@ -1688,12 +1714,33 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         if (c0 > 0) {
             const uint32_t rr = tid >> 4, cc = (tid & 15u) * 4u;
             const unsigned long long *kr = ls.key + rr * kKeyStride + cc;
-            uint32_t m = min(min((uint32_t)(kr[0] >> 32), (uint32_t)(kr[1] >> 32)),
-                             min((uint32_t)(kr[2] >> 32), (uint32_t)(kr[3] >> 32)));
+            uint32_t kz[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) kz[k] = (uint32_t)(kr[k] >> 32);
+            uint32_t m = min(min(kz[0], kz[1]), min(kz[2], kz[3]));
+            // over the tile's pixels inside the frame part only (a partial tile's outside keys stay 0)
+            uint32_t mt = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (tr0 + rr <= tr1 && lx0 + cc + k <= lx1) mt = min(mt, kz[k]);
             for (int o = 2; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+            for (int o = 32; o > 0; o >>= 1) mt = min(mt, (uint32_t)__shfl_xor((int)mt, o));
             if ((tid & 3u) == 0u) ls.zmin[rr][(tid & 15u) >> 2] = m;
+            if (lane == 0u) ls.zwave[wave] = mt;
         }
         __syncthreads();
+        if (c0 > 0) {
+            // the rest of the list starts in the depth bucket of position c0 (buckets run nearest
+            // first): if every pixel of the tile already holds a winner at least as near as that
+            // bucket's ceiling, no listed triangle from here on can win a pixel (strict '>', render.cpp:364)
+            uint32_t b = 0;
+            for (uint32_t k = 1; k < kDepthBuckets; k++) b = ls.bstart[k] <= c0 ? k : b;
+            uint32_t zt = ls.zwave[0];
+            for (uint32_t w = 1; w < kTileThreads / 64u; w++) zt = min(zt, ls.zwave[w]);
+#if !(defined(S3R_TNOSKIP) && S3R_TNOSKIP)
+            if (zt >= bucket_ceiling(b)) break;
+#endif
+        }
 #endif
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
@@ -2150,19 +2197,32 @@ void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, u
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
 uint32_t tile_count(uint32_t W, uint32_t rows_local) { return tile_grid_x(W) * ((rows_local + kTileH - 1) / kTileH); }
+uint64_t tile_slots(uint32_t W, uint32_t rows_local) { return (uint64_t)tile_count(W, rows_local) * kDepthBuckets; }
+
+size_t tile_scan_temp_bytes(uint64_t nslots) {
+    size_t bytes = 0;
+    (void)rocprim::exclusive_scan(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)nslots,
+                                  rocprim::plus<uint32_t>(), nullptr);
+    return bytes;
+}
 size_t raster_rec_bytes() { return sizeof(RasterRec); }
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
-                       uint32_t *offs, uint32_t *cursor, uint32_t *total, hipStream_t st) {
-    const uint32_t nt = tile_count(W, rows_local);
-    (void)hipMemsetAsync(counts, 0, sizeof(uint32_t) * nt, st);
+                       uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
+                       hipStream_t st) {
+    const uint64_t ns = tile_slots(W, rows_local);
+    (void)hipMemsetAsync(counts, 0, sizeof(uint32_t) * ns, st);
     (void)hipMemsetAsync(app_count, 0, sizeof(uint32_t), st);
     if (ntri)
         hipLaunchKernelGGL(k_tile_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor, sw, sh,
                            band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count, counts);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, counts, nt, offs, cursor, total);
+    size_t bytes = scan_temp_bytes;
+    (void)rocprim::exclusive_scan(scan_temp, bytes, (const uint32_t *)counts, offs, 0u, (size_t)ns,
+                                  rocprim::plus<uint32_t>(), st);
+    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
+                       cursor, total);
 }
 
 void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,

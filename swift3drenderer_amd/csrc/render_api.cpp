@@ -111,6 +111,8 @@ struct Dev {
     uint32_t *tile_counts[kSets] = {}, *tile_offs[kSets] = {};
     uint32_t *tile_cursor[kSets] = {}, *tile_total[kSets] = {};
     uint32_t *tile_list[kSets] = {};
+    void *scan_temp = nullptr;                 // rocprim scan of the (tile, bucket) counts
+    size_t scan_temp_bytes = 0;
     void *recs[kSets] = {};        // 2T raster records (positions-only setup)
     uint32_t *boxes[kSets] = {};   // T packed bboxes
     uint32_t *app_list[kSets] = {}, *app_count[kSets] = {};
@@ -538,7 +540,7 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys};
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
@@ -711,7 +713,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         exit(1);
     }
     const float sw = (float)W, sh = (float)H;
-    const uint64_t nt = tile_count(W, rows_local);
+    const uint64_t nt = tile_slots(W, rows_local);          // (tile, depth bucket) entries
     if (d.tiles_cap < nt) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
@@ -720,6 +722,9 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
                 *q = dalloc<uint32_t>(nt);
             }
         }
+        if (d.scan_temp) HIPCHECK(hipFree(d.scan_temp));
+        d.scan_temp_bytes = tile_scan_temp_bytes(nt);
+        d.scan_temp = dalloc<uint8_t>(d.scan_temp_bytes);
         d.tiles_cap = nt;
     }
     const size_t npx = (size_t)W * rows_local;
@@ -746,7 +751,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.boxes[p], d.app_list[p], d.app_count[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
-                      d.tile_total[p], geo);
+                      d.tile_total[p], d.scan_temp, d.scan_temp_bytes, geo);
     // the list size is data-dependent: read it back (the tile path's one host sync per frame)
     uint32_t *host = d.tile_total_host + 2 * p;
     HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));

@@ -66,14 +66,19 @@ void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, u
 // Picks the row path's segment width for a frame of W x rows_local; call before the helpers above.
 void fragment_configure(uint32_t W, uint32_t rows_local);
 
-// Tile path (order-independent fragment stage for many triangles): tiles of 16 local rows x 64 px.
-// recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts/offs/cursor: tile_count().
+// Tile path (order-independent fragment stage for many triangles): tiles of 16 local rows x 64 px,
+// each tile's list split into depth buckets (nearest first; kernels.hip depth_bucket).
+// recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts / offs / cursor:
+// tile_slots() (tile, bucket) entries; scan_temp: tile_scan_temp_bytes(tile_slots()) bytes.
 uint32_t tile_count(uint32_t W, uint32_t rows_local);
+uint64_t tile_slots(uint32_t W, uint32_t rows_local);
+size_t tile_scan_temp_bytes(uint64_t nslots);
 size_t raster_rec_bytes();
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
-                       uint32_t *offs, uint32_t *cursor, uint32_t *total, hipStream_t st);
+                       uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
+                       hipStream_t st);
 void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
                       uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
                       hipStream_t st);
