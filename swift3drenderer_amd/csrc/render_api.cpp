@@ -792,8 +792,13 @@ struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; unsign
 // band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
 // (row path only) `out` is the whole W x H frame in the caller's mapped host buffer: the fragment
 // kernel writes this part's bins at their frame rows -- only the covered ones for host fill.
+//
+// sync (updateAndRender's frames, waited for before the call returns): the geometry runs on `st`
+// itself -- nothing could overlap it, and stream order replaces the cross-stream event (~9 us per
+// frame measured); otherwise it runs on a geometry stream so later frames' geometry overlaps
+// earlier frames' fragment kernels.
 void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                 uint32_t *out, hipStream_t st, const HostFill *hf = nullptr) {
+                 uint32_t *out, hipStream_t st, const HostFill *hf = nullptr, bool sync = false) {
     TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
         render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts);
@@ -842,7 +847,9 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
     const uint32_t p = next_set(d);
-    hipStream_t geo = d.geo[d.frame_no % kGeoStreams];
+    hipStream_t geo = sync && !g.serial ? st : d.geo[d.frame_no % kGeoStreams];
+    const bool chained = geo == st;            // geometry -> fragment by stream order, no event
+    if (chained) follow_previous_frame(d, st);
     d.hp.lap(1);
     // the set's last reader (frame k - kSets) has usually finished: then no cross-stream wait
     if (g.serial) {
@@ -856,17 +863,20 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo,
-                    hf && hf->flags_dev ? nullptr : d.geo_done[p], lpt ? d.order[p] : nullptr);
+                    chained || (hf && hf->flags_dev) ? nullptr : d.geo_done[p], lpt ? d.order[p] : nullptr);
     // host fill: the bins' sky flags to the host as soon as the counts are final (before the
     // fragment kernel, which resets the counts, may start)
-    if (hf && hf->flags_dev) launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, d.geo_done[p]);
+    if (hf && hf->flags_dev)
+        launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, chained ? nullptr : d.geo_done[p]);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
     // only where S3R_SERIAL waits on it.  The fragment workgroups reset their bins' pair counts: the
     // launch is the set's last reader, and the set's next geometry waits for it (wait_set_free).
-    follow_previous_frame(d, st);
-    HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
+    if (!chained) {
+        follow_previous_frame(d, st);
+        HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
+    }
     d.hp.lap(4);
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
@@ -1021,7 +1031,7 @@ void deliver_part(void *arg, int i) {
         }
         if (!job.copy_only)
             render_core(d, job.W, job.H, job.nparts == 1 ? job.H : job.band, job.nparts, (uint32_t)i, rows, d.frame,
-                        d.stream);
+                        d.stream, nullptr, true);
         if (job.nparts == 1) {
             if (job.copy_bytes)
                 HIPCHECK(hipMemcpyAsync(job.host, d.frame, job.copy_bytes, hipMemcpyDeviceToHost, d.stream));
@@ -1205,7 +1215,7 @@ void deliver_part_direct(void *arg, int i) {
         uint32_t *frame_dev = mapped_ptr(d, *dd.reg, job.frame);
         HostFill hf = job.hf[i];
         hf.probe_dev = i == 0 && hf.flags_dev ? frame_dev : nullptr;
-        render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf);
+        render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf, true);
     }
     HIPCHECK(hipStreamSynchronize(d.stream));
 }
