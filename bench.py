@@ -337,7 +337,7 @@ def run_rank0(a, N, np, torch):
         'fps_mean': round(steps / total, 3),
         'frame_GB_per_s': round(frame_bytes / median_s / 1e9, 3),
         'delivery': {'mode': used[0] if len(used) == 1 else used, 'fill_threads': host['fill_threads'],
-                     'link_bytes_per_frame': link_bytes, 'modes': modes},
+                     'fill_gpu_eighths': host['fill_gpu_eighths'], 'link_bytes_per_frame': link_bytes, 'modes': modes},
         'link_roofline': {'bound': 'pcie', 'achieved': round(link_bytes / median_s / 1e9, 2),
                           'peak': LINK_PEAK_GBS * len(devices), 'unit': 'GB/s',
                           'frac': round(link_bytes / median_s / 1e9 / (LINK_PEAK_GBS * len(devices)), 5),

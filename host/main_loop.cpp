@@ -248,14 +248,14 @@ int main(int argc, char **argv) {
     printf("frames %d  mean updateAndRender %.3f ms  median %.3f ms  (%.1f fps, %ux%u)\n", frames,
            frames ? 1e3 * all / frames : 0.0, 1e3 * median, all > 0 ? frames / all : 0.0, pd.width, pd.height);
     if (host_stats) {
-        uint64_t s[11];
+        uint64_t s[12];
         host_stats(s);
         printf("host_stats pinned_frames %llu pageable_frames %llu registrations %llu merges %llu held %llu stale %llu "
-               "copy_frames %llu direct_frames %llu fill_frames %llu fill_threads %llu\n",
+               "copy_frames %llu direct_frames %llu fill_frames %llu fill_threads %llu link_bytes %llu fill_gpu_eighths %llu\n",
                (unsigned long long)s[0], (unsigned long long)s[1], (unsigned long long)s[2],
                (unsigned long long)s[3], (unsigned long long)s[4], (unsigned long long)s[5],
                (unsigned long long)s[6], (unsigned long long)s[7], (unsigned long long)s[8],
-               (unsigned long long)s[9]);
+               (unsigned long long)s[9], (unsigned long long)s[10], (unsigned long long)s[11]);
     }
     if (host_pinned && pd.bufferSize)
         printf("halves_pinned %d %d\n", host_pinned(memory, pd.bufferSize),

@@ -117,22 +117,24 @@ void s3r_unregister_host(void *ptr);
  * {frames delivered into a pinned buffer, frames copied into a pageable one, successful
  * registrations, registrations merged into a larger one, registrations held, stale registrations
  * replaced, frames delivered by copy, by direct writes, by host fill, host fill threads, bytes the
- * devices sent over their PCIe links for the last frame}. */
+ * devices sent over their PCIe links for the last frame, eighths of the sky bins the GPUs write
+ * themselves under host fill}. */
 int s3r_host_pinned(const void *ptr, uint64_t bytes);
-void s3r_host_stats(uint64_t out[11]);
+void s3r_host_stats(uint64_t out[12]);
 
 /* How updateAndRender delivers the frame into a page-locked caller buffer (pixels identical in
  * every mode):
  *   1 copy    render into device memory, then a DMA copy over the PCIe link;
  *   2 direct  the fragment kernel writes the pixels straight into the caller's buffer;
- *   3 fill    host fill: the GPU writes only the bins some triangle meets, and `fill_threads`
- *             library threads write the background of the others (render.cpp:282's fill)
- *             meanwhile, so the link carries the covered bins only;
- *   0 auto    (default) host fill on up to 2 devices, direct beyond; -1: S3R_DELIVERY
- *             (copy|direct|fill|auto) or auto.
+ *   3 fill    host fill: the GPU writes the bins and row chunks some triangle covers, library threads
+ *             write the background of the rest (render.cpp:282's fill) meanwhile, so the link
+ *             carries mostly covered pixels; adaptive: a share of the background bins goes back to
+ *             the GPU(s) whenever the threads finish after the devices (S3R_FILL_GPU=0..8 fixes the
+ *             share in eighths);
+ *   0 auto    (default) host fill; -1: S3R_DELIVERY (copy|direct|fill|auto) or auto.
  * Tile-path frames and buffers that cannot be page-locked are always copied.  fill_threads -1:
- * S3R_FILL_THREADS or 4.  Returns 0, or -1 on a bad mode or thread count (0 or > 64).
- * s3r_delivery() returns the mode in effect (0-3). */
+ * S3R_FILL_THREADS, or 4 (one device) / 8 (several).  Returns 0, or -1 on a bad mode or thread
+ * count (0 or > 64).  s3r_delivery() returns the mode in effect (0-3). */
 int s3r_set_delivery(int mode, int fill_threads);
 int s3r_delivery(void);
 

@@ -1022,9 +1022,10 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     const size_t orow = (size_t)(HOSTW ? y : lr) * W;
     if (npairs == 0) {
         // no triangle meets this block (sky): background only (render.cpp:282), 16 B per lane where
-        // the row segment is 16-B aligned -- unless the host fills sky bins (host_fill: the frame is
-        // the caller's host buffer, k_sky_flags told the host which bins are sky)
-        if (row_ok && !host_fill) {
+        // the row segment is 16-B aligned -- unless the host fills this sky bin (host_fill = 1 +
+        // gpu_eighths: the frame is the caller's host buffer; k_sky_flags gave the sky bins with
+        // bid % 8 >= gpu_eighths to the host and kept the others for the GPU)
+        if (row_ok && (!host_fill || (bid & 7u) < host_fill - 1u)) {
             uint32_t *seg = out + orow + xs;
             const uint32_t n = xe - xs + 1u;
             if ((orow + xs) % 4u == 0u) {
@@ -2141,7 +2142,7 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
-                     bool frame_rows, bool host_fill, unsigned long long *chunk_flags, uint32_t fill_tag) {
+                     bool frame_rows, uint32_t host_fill, unsigned long long *chunk_flags, uint32_t fill_tag) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2159,11 +2160,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, (uint32_t)host_fill, chunk_flags, fill_tag);
+                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           (uint32_t)host_fill, chunk_flags, fill_tag);
+                           host_fill, chunk_flags, fill_tag);
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in
@@ -2171,11 +2172,13 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
 // background of sky bins while k_fragment writes only the covered bins into the caller's buffer.
 // probe (may be null): the device address of the caller's pixel 0; the magic written there before
 // bin 0's flag (release) lets the host check that the mapping reaches the caller's pages.
+// gpu_eighths: sky bins with b % 8 below it are written by the fragment kernel (kGpuBit), the rest by
+// the host (kSkyBit) -- the host / link balance of render_api.cpp's adaptive host fill.
 __global__ void __launch_bounds__(256) k_sky_flags(const uint32_t *__restrict__ bincnt, uint32_t nbins, uint32_t *flags,
-                                                   uint32_t tag, uint32_t *probe) {
+                                                   uint32_t tag, uint32_t *probe, uint32_t gpu_eighths) {
     const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     if (b >= nbins) return;
-    const uint32_t f = bincnt[b] == 0u ? (tag | kSkyBit) : tag;
+    const uint32_t f = bincnt[b] != 0u ? tag : ((b & 7u) < gpu_eighths ? (tag | kGpuBit) : (tag | kSkyBit));
     if (b == 0 && probe) {
         __hip_atomic_store(probe, kMapProbe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(flags, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2185,14 +2188,14 @@ __global__ void __launch_bounds__(256) k_sky_flags(const uint32_t *__restrict__ 
 }
 
 void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, uint32_t tag, uint32_t *probe,
-                      hipStream_t st, hipEvent_t done) {
+                      uint32_t gpu_eighths, hipStream_t st, hipEvent_t done) {
     const uint32_t blocks = (uint32_t)((nbins + 255) / 256);
     if (blocks == 0) {
         if (done) (void)hipEventRecord(done, st);
         return;
     }
     hipExtLaunchKernelGGL(k_sky_flags, dim3(blocks), dim3(256), 0, st, nullptr, done, 0, bincnt, (uint32_t)nbins, flags,
-                          tag, probe);
+                          tag, probe, gpu_eighths);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

@@ -302,6 +302,10 @@ struct Lib {
     int fill_threads = -1;                     // host fill threads; -1: S3R_FILL_THREADS or the default
     Pool fill_pool;
     uint64_t copy_frames = 0, direct_frames = 0, fill_frames = 0;
+    // adaptive host fill: eighths of the sky bins the GPUs write themselves, and the smoothed
+    // (fill threads' finish - devices' finish) in microseconds that steers it
+    int fill_gpu = -1;
+    double fill_skew_us = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
 
@@ -786,7 +790,13 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
 // with flags_dev (host fill) the sky-flag kernel publishes the bins' flags with this tag, and the
 // fragment kernel leaves sky bins and, in covered bins, the row chunks without a winner to the host
 // (their masks in chunks_dev); without, the fragment kernel writes every pixel.
-struct HostFill { uint32_t *flags_dev; uint32_t tag; uint32_t *probe_dev; unsigned long long *chunks_dev; };
+struct HostFill {
+    uint32_t *flags_dev;
+    uint32_t tag;
+    uint32_t *probe_dev;
+    unsigned long long *chunks_dev;
+    uint32_t gpu_eighths;     // sky bins with bin % 8 below this stay with the GPU (adaptive split)
+};
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
 // band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
@@ -867,7 +877,8 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     // host fill: the bins' sky flags to the host as soon as the counts are final (before the
     // fragment kernel, which resets the counts, may start)
     if (hf && hf->flags_dev)
-        launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, geo, chained ? nullptr : d.geo_done[p]);
+        launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, hf->gpu_eighths, geo,
+                         chained ? nullptr : d.geo_done[p]);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
@@ -881,8 +892,8 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
-                    lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev, hf ? hf->chunks_dev : nullptr,
-                    hf ? hf->tag : 0u);
+                    lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev ? 1u + hf->gpu_eighths : 0u,
+                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -1056,12 +1067,15 @@ void deliver_part(void *arg, int i) {
 //           soon as its geometry is done (k_sky_flags), writes only its covered bins, and the
 //           library's fill threads write the sky bins' background with streaming stores meanwhile.
 //           The link carries the covered bins only; the host's memory writes overlap the GPU's.
-// Auto: host fill for up to kFillMaxParts devices (one link carries the frame: halving its bytes
-// matters most), direct beyond (N links carry the frame, and host fill would put the sky bins of
-// every part on the host's memory bandwidth).  Tile-path frames and buffers that cannot be
-// page-locked are copied.
-constexpr int kDefaultFillThreads = 4;     // measured: 2 CPU-bound, 8-16 add scheduling jitter (p90)
-constexpr uint32_t kFillMaxParts = 2;
+// The host fill is adaptive: with N devices the links carry N times the bytes of one while the fill
+// threads' memory bandwidth stays what it is, so k_sky_flags leaves g/8 of the sky bins (bin % 8 < g)
+// to the GPUs, and after every frame g moves one step towards balance -- up when the fill threads
+// finished later than the devices (smoothed, beyond a dead band), down when the devices did.  Any g
+// gives the same pixels; g = 8 is direct delivery plus the flags.  S3R_FILL_GPU=g fixes it.
+// Auto = host fill.  Tile-path frames and buffers that cannot be page-locked are copied.
+constexpr int kDefaultFillThreads = 4;     // one device; measured: 2 CPU-bound, 8-16 add scheduling jitter (p90)
+constexpr int kDefaultFillThreadsMulti = 8;
+constexpr double kFillDeadbandUs = 15.0;
 enum Delivery_ { kAuto = 0, kCopy = 1, kDirect = 2, kFill = 3 };
 
 int delivery_mode() {
@@ -1075,13 +1089,16 @@ int delivery_mode() {
 
 constexpr uint32_t kFillBlock = 8;            // bins per fill-thread work block (contiguous: whole lines)
 
-int fill_threads() {
+// Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override).
+int fill_threads(uint32_t nparts = 1) {
     if (g.fill_threads < 0) {
-        const char *e = getenv("S3R_FILL_THREADS");
-        const int v = e ? atoi(e) : kDefaultFillThreads;
-        g.fill_threads = v < 1 ? 1 : (v > 64 ? 64 : v);
+        if (const char *e = getenv("S3R_FILL_THREADS")) {
+            const int v = atoi(e);
+            g.fill_threads = v < 1 ? 1 : (v > 64 ? 64 : v);
+        }
     }
-    return g.fill_threads;
+    if (g.fill_threads > 0) return g.fill_threads;
+    return nparts > 1 ? kDefaultFillThreadsMulti : kDefaultFillThreads;
 }
 
 struct FillPart {
@@ -1099,7 +1116,15 @@ struct FillJob {
     HostFill hf[kMaxDevices];
     std::atomic<bool> stale{false};  // pixel 0 checked before its bin was filled: the mapping is stale
     std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
+    std::chrono::steady_clock::time_point t0;
+    std::atomic<int64_t> dev_end_ns{0}, fill_end_ns{0};   // latest finish of a device part / a fill thread
 };
+
+void note_end(const FillJob &job, std::atomic<int64_t> &end) {
+    const int64_t t = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
+    int64_t cur = end.load(std::memory_order_relaxed);
+    while (t > cur && !end.compare_exchange_weak(cur, t, std::memory_order_relaxed)) {}
+}
 
 // Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
 // row_in_bin * chunks_per_row + chunk) of a covered bin; returns the pixels written.
@@ -1159,7 +1184,8 @@ void fill_worker(void *arg, int idx) {
             uint32_t mask = 0;
             if (!(e & kWaitChunks)) {
                 const uint32_t f = __atomic_load_n(fp.flags + b, __ATOMIC_ACQUIRE);
-                if ((f & ~kSkyBit) != fp.tag) { pend[keep++] = e; continue; }
+                if ((f & ~(kSkyBit | kGpuBit)) != fp.tag) { pend[keep++] = e; continue; }
+                if (f & kGpuBit) continue;                      // a sky bin the GPU writes itself
                 if (!(f & kSkyBit)) { pend[keep++] = e | kWaitChunks; continue; }
                 sky = true;
             } else {
@@ -1185,6 +1211,7 @@ void fill_worker(void *arg, int idx) {
     }
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
+    note_end(job, job.fill_end_ns);
 }
 
 // The device address of host buffer p inside registration r on device d (cached per registration).
@@ -1218,6 +1245,7 @@ void deliver_part_direct(void *arg, int i) {
         render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf, true);
     }
     HIPCHECK(hipStreamSynchronize(d.stream));
+    note_end(job, job.dev_end_ns);
 }
 
 // One updateAndRender frame by direct delivery or host fill (fill).  Returns false if the caller's
@@ -1230,7 +1258,12 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
     job.W = W;
     job.H = H;
     job.nparts = (int)nparts;
-    job.threads = fill ? fill_threads() : 0;
+    job.threads = fill ? fill_threads(nparts) : 0;
+    if (fill && g.fill_gpu < 0) {
+        const char *e = getenv("S3R_FILL_GPU");
+        g.fill_gpu = e ? atoi(e) : (int)(2 * (nparts - 1));
+        g.fill_gpu = g.fill_gpu < 0 ? 0 : (g.fill_gpu > 8 ? 8 : g.fill_gpu);
+    }
     if (fill && g.fill_pool.workers() != job.threads) g.fill_pool.start(job.threads);
     const uint32_t band = nparts == 1 ? H : g.band;
     for (uint32_t i = 0; i < nparts; i++) {
@@ -1242,7 +1275,7 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
         fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
         if (!fill) {
-            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr};
+            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0};
             continue;
         }
         if (d.fill_cap < fp.bins) {
@@ -1259,7 +1292,7 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
             d.fill_cap = fp.bins;
             d.fill_tag = 0;
         }
-        if (++d.fill_tag >= kSkyBit) {                 // (after 2^31 frames) restart the tags
+        if (++d.fill_tag >= kGpuBit) {                 // (after 2^30 frames) restart the tags
             memset(d.fill_flags, 0, d.fill_cap * sizeof(uint32_t));
             memset(d.fill_chunks, 0, d.fill_cap * sizeof(unsigned long long));
             d.fill_tag = 1;
@@ -1267,19 +1300,28 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
         fp.flags = d.fill_flags;
         fp.chunks = d.fill_chunks;
         fp.tag = d.fill_tag;
-        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev};
+        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
     DirectDelivery dd{&job, reg};
+    job.t0 = std::chrono::steady_clock::now();
     if (fill) g.fill_pool.launch(fill_worker, &job, job.threads + 1);
     g.pool.run(deliver_part_direct, &dd, (int)nparts);
     if (fill) g.fill_pool.join();
+    if (fill && !getenv("S3R_FILL_GPU")) {
+        // one step towards balance between the fill threads and the devices
+        const double skew = (double)(job.fill_end_ns.load() - job.dev_end_ns.load()) / 1e3;
+        g.fill_skew_us = 0.75 * g.fill_skew_us + 0.25 * skew;
+        if (g.fill_skew_us > kFillDeadbandUs && g.fill_gpu < 8) { g.fill_gpu++; g.fill_skew_us = 0; }
+        else if (g.fill_skew_us < -kFillDeadbandUs && g.fill_gpu > 0) { g.fill_gpu--; g.fill_skew_us = 0; }
+    }
     // pixel 0 written by the GPU (direct, or a covered chunk under host fill) is a pixel, neither
     // probe, unless the mapping is stale; a pixel 0 the host filled was checked by its fill thread
     bool host0 = false;
     if (fill && job.parts[0].bins) {
-        host0 = (job.parts[0].flags[0] & kSkyBit) || (job.parts[0].chunks[0] & 1ull);
+        const uint32_t f0 = job.parts[0].flags[0];
+        host0 = (f0 & kSkyBit) || (!(f0 & kGpuBit) && (job.parts[0].chunks[0] & 1ull));
     }
     const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
     (fill ? g.fill_frames : g.direct_frames)++;
@@ -1310,7 +1352,7 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     if (pinned && npx && copy_bytes == frame_bytes && mode != kCopy && !use_tile_path()) {
         // direct / host fill: the GPU(s) write straight into the buffer (host fill: covered bins only,
         // the sky bins by the host)
-        const bool fill = mode == kFill || (mode == kAuto && nparts <= kFillMaxParts);
+        const bool fill = mode == kFill || mode == kAuto;
         if (mapped_frame(pixel_data->buffer, W, H, nparts, fill)) {
             g.pinned_frames++;
             for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
@@ -1454,7 +1496,7 @@ __attribute__((visibility("default"))) int s3r_host_pinned(const void *ptr, uint
     return r && r->ok ? 1 : 0;
 }
 
-__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[11]) {
+__attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[12]) {
     out[0] = g.pinned_frames;
     out[1] = g.pageable_frames;
     out[2] = g.registrations;
@@ -1464,8 +1506,9 @@ __attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[11]) {
     out[6] = g.copy_frames;
     out[7] = g.direct_frames;
     out[8] = g.fill_frames;
-    out[9] = (uint64_t)fill_threads();
+    out[9] = (uint64_t)fill_threads(g.devs.size() > 1 ? (uint32_t)g.devs.size() : 1u);
     out[10] = g.link_bytes;
+    out[11] = g.fill_gpu < 0 ? 0 : (uint64_t)g.fill_gpu;
 }
 
 __attribute__((visibility("default"))) int s3r_set_delivery(int mode, int fill_threads) {

@@ -12,15 +12,16 @@ namespace s3r {
 // Renders `rows_local` rows: local row lr is frame row ((lr / band) * nparts + part) * band + lr % band
 // (interleaved row bands; nparts = 1, band = H renders the whole frame).  Output is compact,
 // out[lr * W + x], or with frame_rows the whole frame's row, out[y * W + x] (out = a W x H frame, e.g.
-// the caller's host buffer).  host_fill: sky bins (no triangle) write nothing -- the host fills them
-// (launch_sky_flags) -- and neither do the row chunks of covered bins that end without a winner:
+// the caller's host buffer).  host_fill = 1 + g (0: off): sky bins (no triangle) with bin % 8 >= g
+// write nothing -- the host fills them (launch_sky_flags) -- and neither do the row chunks of covered
+// bins that end without a winner:
 // each bin's workgroup stores chunk_flags[bin] = (fill_tag << 32) | mask at its end, bit
 // (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
-                     bool frame_rows = false, bool host_fill = false, unsigned long long *chunk_flags = nullptr,
+                     bool frame_rows = false, uint32_t host_fill = 0, unsigned long long *chunk_flags = nullptr,
                      uint32_t fill_tag = 0);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
@@ -59,10 +60,13 @@ FragLayout fragment_layout(uint32_t W, uint32_t rows_local);
 // probe (may be null): device address of the caller's pixel 0, set to kMapProbe before flags[0] is
 // published (the host's check that the mapping of its buffer is not stale).  Neither value is a
 // pixel (pixels are 0x00RRGGBB).
+// gpu_eighths: sky bins with bin % 8 < gpu_eighths stay with the GPU (flag tag | kGpuBit: the fragment
+// kernel writes their background); tags stay below kGpuBit.
 constexpr uint32_t kSkyBit = 0x80000000u;
+constexpr uint32_t kGpuBit = 0x40000000u;
 constexpr uint32_t kMapProbe = 0xFEA5A5A5u;
 void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, uint32_t tag, uint32_t *probe,
-                      hipStream_t st, hipEvent_t done);
+                      uint32_t gpu_eighths, hipStream_t st, hipEvent_t done);
 // Picks the row path's segment width for a frame of W x rows_local; call before the helpers above.
 void fragment_configure(uint32_t W, uint32_t rows_local);
 

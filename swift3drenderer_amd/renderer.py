@@ -116,10 +116,10 @@ class Renderer:
         return bool(self.lib.s3r_host_pinned(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
 
     def host_stats(self) -> dict:
-        out = (ctypes.c_uint64 * 11)()
+        out = (ctypes.c_uint64 * 12)()
         self.lib.s3r_host_stats(out)
         keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale', 'copy_frames',
-                'direct_frames', 'fill_frames', 'fill_threads', 'link_bytes')
+                'direct_frames', 'fill_frames', 'fill_threads', 'link_bytes', 'fill_gpu_eighths')
         return dict(zip(keys, (int(v) for v in out)))
 
     DELIVERIES = {'env': -1, 'auto': 0, 'copy': 1, 'direct': 2, 'fill': 3}

@@ -176,7 +176,7 @@ def test_delivery_modes_match_oracle(multi, scene_dir, mode, fill, devices):
         frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', 1920, 1080), devices)
         frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_id', 3840, 2160, extra=1), devices)
         st = multi.host_stats()                      # (counters restart at each configure)
-        used = mode if mode != 'auto' else ('fill' if len(devices) <= 2 else 'direct')
+        used = mode if mode != 'auto' else 'fill'
         assert st[f'{used}_frames'] == 2 and st['pinned_frames'] == 2, st
         assert multi.delivery() == mode
     finally:
@@ -193,3 +193,20 @@ def test_host_fill_sparse_and_empty_frames(multi, scene_dir, tmp_path):
     away = [(640, 480, (0, 0, 0, 0, 0, 0)), (640, 480, (0, 0, 0, 0, 4000.0, 0.0)), (640, 480, (0, 0, 0, 0, 8000.0, 0.0))]
     frames_vs_oracle(multi, scene_dir['full'], away, [0, 0])
     assert multi.host_stats()['fill_frames'] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('split', [0, 3, 8])
+@pytest.mark.parametrize('devices', [[0], [0, 0]])
+def test_host_fill_split_matches_oracle(multi, scene_dir, monkeypatch, split, devices):
+    """Host fill with a fixed share of the sky bins (S3R_FILL_GPU eighths) written by the GPU instead
+    of the fill threads -- the adaptive split's every position gives the oracle's frames."""
+    monkeypatch.setenv('S3R_FILL_GPU', str(split))
+    multi.set_delivery('fill')
+    try:
+        frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', 1920, 1080), devices)
+        frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_clip', 3840, 2160, extra=1), devices)
+        st = multi.host_stats()
+        assert st['fill_gpu_eighths'] == split and st['fill_frames'] == 3, st
+    finally:
+        multi.set_delivery('env')
