@@ -3,7 +3,7 @@
 //   k_geometry  render.cpp:284-359, :374-379  per (slot, row block): vertex + normal transform of the
 //                                   slot's corners, reject, near-plane clip (:212-262), cull, raster
 //                                   setup (slot t, or slot T+t for a clip split); the fragment
-//                                   workgroups' slot masks; exact row and segment starts.
+//                                   workgroups' pair records; exact row and segment starts.
 //   k_fragment  render.cpp:360-382  one wave per (row, 64*NCH-pixel segment).  Triangles are taken
 //                                   in slot order, 64 at a time: lanes first act as TRIANGLES and
 //                                   walk each triangle's exact barycentric sequence to this row
@@ -519,9 +519,10 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
 // workgroup per (slot, block of kGeoRows local rows) x 3 components.
 //   * thread 0 sets the slot up (geo_slot_setup: transform, reject, clip, cull, raster setup,
 //     render.cpp:285-359); the row-block-0 workgroup stores the slot's TriSetup record;
-//   * bins: the slot's bit is set in the slot mask of every fragment workgroup (kWaves local rows x
-//     one segment) its bbox meets -- the fragment kernel reads the set bits in slot order, i.e. the
-//     reference's processing order, and clears them for the buffer's next frame;
+//   * bins: the slot reserves a pair record (atomicAdd on the bin's count) in every fragment
+//     workgroup's bin (kWaves local rows x one segment) its bbox meets and writes its raster
+//     constants and walk state there -- the fragment workgroup ranks its pairs by slot (the
+//     reference's processing order) and resets the count for the buffer set's next frame;
 //   * starts: lane (row, component) walks the reference's sequence exactly (exact_walk): wy += dy
 //     down to its row (render.cpp:378), then w += dx along the row through every fragment-segment
 //     boundary inside the bbox (:374), storing the row start and each segment start.

@@ -184,7 +184,7 @@ def stacked_quads_scene(path, n=160, size=1.0):
 
 def test_row_path_list_overflow(gpu_renderer, tmp_path):
     """320 stacked triangles cover every fragment workgroup: more than the 128 a workgroup lists from
-    the geometry's slot masks, so the row path takes its in-kernel slot-scan rounds (build_list)."""
+    its bin's pair records (kPairMax), so the row path takes its in-kernel slot-scan rounds (build_list)."""
     path = str(tmp_path / 'stack.bin')
     stacked_quads_scene(path)
     for w, h in ((320, 240), (1280, 720)):

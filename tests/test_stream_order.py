@@ -2,7 +2,8 @@
 
 * frames alternating between the null (legacy default) stream, a side stream and updateAndRender's
   own stream are ordered (follow_previous_frame: a switch from or to NULL needs the hand-off event);
-* the slot-mask / order buffers regrow between two frames issued back to back without a sync;
+* the bin (pair count / pair record) and order buffers regrow between two frames issued back to
+  back without a sync;
 * the uint32 frame tags restart before they wrap (restart_tags);
 * a host buffer freed and reallocated at the same address still receives the frame.
 """
@@ -64,8 +65,8 @@ def test_null_stream_then_side_stream(gpu_renderer, scene_dir, path):
 
 @pytest.mark.parametrize('path', ['rows', 'tiles'])
 def test_regrow_back_to_back(gpu_renderer, scene_dir, monkeypatch, path):
-    """A small frame, then larger ones issued immediately on the same side stream: the slot masks, the
-    longest-first order buffers (forced on) and the tile buffers are reallocated between frames in
+    """A small frame, then larger ones issued immediately on the same side stream: the bins' pair
+    counts and records, the longest-first order buffers (forced on) and the tile buffers are reallocated between frames in
     flight; the first frame after each regrow equals the oracle's."""
     import torch
     monkeypatch.setenv('S3R_LPT_MIN', '0')
