@@ -1544,12 +1544,26 @@ __device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSe
     q[3] = make_float4(t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]);
 }
 
+// Vertex stage (render.cpp:285-289 as a pass over the vertex stream, north_star's "vertex-stage
+// kernel"; S3R_VERTEX_STAGE=1): every vertex transformed and projected once, coalesced, into
+// rv[i] = (raster x, y, z, 0); k_tile_setup<true> then gathers three of those per triangle instead of
+// transforming its three corners (an icosahedron vertex is a corner of five triangles).
+__global__ void __launch_bounds__(256) k_tile_vertex(const float4 *__restrict__ vtx, uint32_t nv, Mat34 m, float factor,
+                                                     float half_w, float half_h, float4 *__restrict__ rv) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= nv) return;
+    Vert d;
+    load_corner(vtx, i, m, factor, half_w, half_h, d);
+    rv[i] = make_float4(d.rv.x, d.rv.y, d.rv.z, 0.0f);
+}
+
+template <bool VS>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, Mat34 m, float factor, float sw, float sh,
                                                     uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                     RasterRec *__restrict__ recs, uint32_t *__restrict__ boxes,
                                                     uint32_t *__restrict__ app_list, uint32_t *__restrict__ app_count,
-                                                    uint32_t *__restrict__ counts) {
+                                                    uint32_t *__restrict__ counts, const float4 *__restrict__ vrv) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = t < ntri;
     const float half_w = sw / 2, half_h = sh / 2;
@@ -1557,14 +1571,26 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     TriSetup ts;
     bool live = false;
     if (in) {
+        uint32_t vi[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
+            vi[k] = vidx[3 * t + k];
+            if (VS) {
+                const float4 r = vrv[vi[k]];                                   // the vertex stage's rv
+                d[k].rv = mk3(r.x, r.y, r.z);
+                d[k].cv = mk3(0, 0, 0);
+            } else {
+                load_corner(vtx, vi[k], m, factor, half_w, half_h, d[k]);
+            }
             d[k].n = mk3(0, 0, 0);
             d[k].pay = make_float4(0, 0, 0, 0);
         }
         if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
             if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear) {               // :308, rare
+                if (VS) {                         // the clip needs camera-space corners: recompute
+#pragma unroll
+                    for (int k = 0; k < 3; k++) load_corner(vtx, vi[k], m, factor, half_w, half_h, d[k]);
+                }
                 Vert app[3];
                 uint32_t app_first = 0;
                 // positions do not depend on the colour / texture payload (clip's `textured`)
@@ -2215,13 +2241,22 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
                        uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
-                       hipStream_t st) {
+                       hipStream_t st, float4 *vrv, uint32_t nv) {
     const uint64_t ns = tile_slots(W, rows_local);
     (void)hipMemsetAsync(counts, 0, sizeof(uint32_t) * ns, st);
     (void)hipMemsetAsync(app_count, 0, sizeof(uint32_t), st);
-    if (ntri)
-        hipLaunchKernelGGL(k_tile_setup, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor, sw, sh,
-                           band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count, counts);
+    if (vrv && nv)
+        hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv);
+    if (ntri) {
+        if (vrv)
+            hipLaunchKernelGGL(k_tile_setup<true>, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor,
+                               sw, sh, band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count,
+                               counts, (const float4 *)vrv);
+        else
+            hipLaunchKernelGGL(k_tile_setup<false>, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor,
+                               sw, sh, band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count,
+                               counts, (const float4 *)nullptr);
+    }
     size_t bytes = scan_temp_bytes;
     (void)rocprim::exclusive_scan(scan_temp, bytes, (const uint32_t *)counts, offs, 0u, (size_t)ns,
                                   rocprim::plus<uint32_t>(), st);

@@ -113,6 +113,7 @@ struct Dev {
     uint32_t *tile_list[kSets] = {};
     void *scan_temp = nullptr;                 // rocprim scan of the (tile, bucket) counts
     size_t scan_temp_bytes = 0;
+    float4 *vrv = nullptr;                     // tile path vertex stage (S3R_VERTEX_STAGE): projected vertices
     void *recs[kSets] = {};        // 2T raster records (positions-only setup)
     uint32_t *boxes[kSets] = {};   // T packed bboxes
     uint32_t *app_list[kSets] = {}, *app_count[kSets] = {};
@@ -544,7 +545,7 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp};
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
@@ -738,6 +739,18 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         d.keys = dalloc<unsigned long long>(npx);
         d.keys_cap = npx;
     }
+    // vertex stage (k_tile_vertex): measured on the 20 M-triangle stress scene at 4K, part 0 of 8
+    // 1 996 -> 2 108 fps (setup 307 -> 235 us + 57 us for the stage), whole frame 826 -> 808 fps: on
+    // for frame parts, where the per-triangle setup is replicated on every device; S3R_VERTEX_STAGE
+    // = 0 / 1 forces it
+    const char *vs_env = getenv("S3R_VERTEX_STAGE");
+    if (vs_env ? atoi(vs_env) != 0 : nparts > 1) {
+        if (!d.vrv) d.vrv = dalloc<float4>(g.nv);
+    } else if (d.vrv) {
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipFree(d.vrv));
+        d.vrv = nullptr;
+    }
     if (!d.recs[0]) {
         for (int p = 0; p < kSets; p++) {
             d.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
@@ -755,7 +768,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.boxes[p], d.app_list[p], d.app_count[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
-                      d.tile_total[p], d.scan_temp, d.scan_temp_bytes, geo);
+                      d.tile_total[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv);
     // the list size is data-dependent: read it back (the tile path's one host sync per frame)
     uint32_t *host = d.tile_total_host + 2 * p;
     HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));

@@ -82,7 +82,9 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
                        uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
-                       hipStream_t st);
+                       hipStream_t st, float4 *vrv = nullptr, uint32_t nv = 0);
+// vrv (nv float4, may be null): run the vertex stage first (k_tile_vertex) and set triangles up
+// from its projected vertices.
 void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
                       uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
                       hipStream_t st);

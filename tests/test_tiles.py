@@ -149,3 +149,21 @@ def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
     finally:
         gpu_renderer.set_raster_path('auto')
     assert np.array_equal(a, b), diff(a, b)
+
+
+@pytest.mark.parametrize('case', [('full', 'P_clip', 640, 480), ('full', 'P_over', 1000, 333), ('stress', 'P_id', 1920, 1080),
+                                  ('stress', 'P_strafe', 1280, 720)])
+def test_vertex_stage_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeypatch, case):
+    """The tile path with the vertex stage (S3R_VERTEX_STAGE=1: every vertex projected once by
+    k_tile_vertex, triangles set up from those; the near-plane clip recomputes its corners)."""
+    monkeypatch.setenv('S3R_VERTEX_STAGE', '1')
+    name, pose, w, h = case
+    path = icosa_dir[2000] if name == 'stress' else scene_dir[name]
+    gpu_renderer.set_raster_path('tiles')
+    try:
+        script = poses.script(pose)
+        want = oracle_render_pose(path, script, w, h, extra_frames=1)
+        got = render_pose(gpu_renderer, path, script, w, h, extra_frames=1)
+        assert np.array_equal(got, want), diff(got, want)
+    finally:
+        gpu_renderer.set_raster_path('auto')
