@@ -19,6 +19,7 @@
 // devices' HIP calls do not serialise.  The call returns when every part has landed.
 #include <dlfcn.h>
 #include <limits.h>
+#include <sched.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -307,6 +308,7 @@ struct Lib {
     // (fill threads' finish - devices' finish) in microseconds that steers it
     int fill_gpu = -1;
     double fill_skew_us = 0;
+    bool unmapped = false;                     // a device could not map a caller buffer: copy only
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
 
@@ -1102,7 +1104,29 @@ int delivery_mode() {
 
 constexpr uint32_t kFillBlock = 8;            // bins per fill-thread work block (contiguous: whole lines)
 
-// Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override).
+// CPUs this process may keep busy: its affinity mask, capped by a cgroup v2 CPU quota (cpu.max,
+// e.g. "1600000 100000" = 16 CPUs).  Busy threads beyond a quota get the whole process throttled.
+int available_cpus() {
+    static int n = -1;
+    if (n >= 0) return n;
+    cpu_set_t set;
+    n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 64;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long period = 0;
+        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long quota = atol(q);
+            const int c = (int)(quota / period);
+            if (c > 0 && c < n) n = c;
+        }
+        fclose(f);
+    }
+    return n;
+}
+
+// Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override):
+// by default 4 (one device) or 8, but no more than the CPUs left beside the calling thread and the
+// nparts - 1 device workers.
 int fill_threads(uint32_t nparts = 1) {
     if (g.fill_threads < 0) {
         if (const char *e = getenv("S3R_FILL_THREADS")) {
@@ -1111,7 +1135,9 @@ int fill_threads(uint32_t nparts = 1) {
         }
     }
     if (g.fill_threads > 0) return g.fill_threads;
-    return nparts > 1 ? kDefaultFillThreadsMulti : kDefaultFillThreads;
+    const int want = nparts > 1 ? kDefaultFillThreadsMulti : kDefaultFillThreads;
+    const int spare = available_cpus() - (int)nparts - 1;
+    return want < spare ? want : (spare > 1 ? spare : 1);
 }
 
 struct FillPart {
@@ -1228,20 +1254,24 @@ void fill_worker(void *arg, int idx) {
 }
 
 // The device address of host buffer p inside registration r on device d (cached per registration).
+// Null if this device has no mapping of the registration (the frame is then delivered by copy).
 uint32_t *mapped_ptr(Dev &d, const Lib::Reg &r, void *p) {
     if (d.map_epoch != g.reg_epoch || d.map_host != r.a) {
         void *dp = nullptr;
-        HIPCHECK(hipHostGetDevicePointer(&dp, (void *)r.a, 0));
+        if (hipHostGetDevicePointer(&dp, (void *)r.a, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            dp = nullptr;
+        }
         d.map_host = r.a;
         d.map_dev = (uintptr_t)dp;
         d.map_epoch = g.reg_epoch;
     }
-    return (uint32_t *)(d.map_dev + ((uintptr_t)p - r.a));
+    return d.map_dev ? (uint32_t *)(d.map_dev + ((uintptr_t)p - r.a)) : nullptr;
 }
 
 struct DirectDelivery {
     FillJob *job;
-    const Lib::Reg *reg;
+    uint32_t *frame_dev[kMaxDevices];    // each device's address of the caller's buffer
 };
 
 // Part i of a direct / host-fill frame on device i: render it into the caller's mapped buffer.
@@ -1252,7 +1282,7 @@ void deliver_part_direct(void *arg, int i) {
     HIPCHECK(hipSetDevice(d.device));
     const FillPart &fp = job.parts[i];
     if (fp.rows_local && job.W) {
-        uint32_t *frame_dev = mapped_ptr(d, *dd.reg, job.frame);
+        uint32_t *frame_dev = dd.frame_dev[i];
         HostFill hf = job.hf[i];
         hf.probe_dev = i == 0 && hf.flags_dev ? frame_dev : nullptr;
         render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf, true);
@@ -1261,11 +1291,24 @@ void deliver_part_direct(void *arg, int i) {
     note_end(job, job.dev_end_ns);
 }
 
-// One updateAndRender frame by direct delivery or host fill (fill).  Returns false if the caller's
-// registration turned out to be stale (the frame did not reach the caller's pages: the caller redoes
-// it by copy).
-bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, bool fill) {
+// One updateAndRender frame by direct delivery or host fill (fill).  kStaleMap: the caller's
+// registration turned out to be stale (the frame did not reach the caller's pages); kUnmapped: a
+// device has no mapping of the buffer (nothing was rendered) -- either way the caller redoes the
+// frame by copy.
+enum MappedResult { kMapped, kStaleMap, kUnmapped };
+
+MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, bool fill) {
     const Lib::Reg *reg = find_reg(buffer, (size_t)W * H * 4);
+    DirectDelivery dd{};
+    for (uint32_t i = 0; i < nparts; i++) {
+        Dev &d = *g.devs[i];
+        HIPCHECK(hipSetDevice(d.device));
+        dd.frame_dev[i] = reg ? mapped_ptr(d, *reg, buffer) : nullptr;
+        if (!dd.frame_dev[i]) {
+            HIPCHECK(hipSetDevice(g.devs[0]->device));
+            return kUnmapped;
+        }
+    }
     FillJob job;
     job.frame = buffer;
     job.W = W;
@@ -1317,7 +1360,7 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
-    DirectDelivery dd{&job, reg};
+    dd.job = &job;
     job.t0 = std::chrono::steady_clock::now();
     if (fill) g.fill_pool.launch(fill_worker, &job, job.threads + 1);
     g.pool.run(deliver_part_direct, &dd, (int)nparts);
@@ -1339,7 +1382,7 @@ bool mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, boo
     const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
     (fill ? g.fill_frames : g.direct_frames)++;
     g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load());
-    return !stale;
+    return stale ? kStaleMap : kMapped;
 }
 
 }  // namespace
@@ -1366,16 +1409,22 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
         // direct / host fill: the GPU(s) write straight into the buffer (host fill: covered bins only,
         // the sky bins by the host)
         const bool fill = mode == kFill || mode == kAuto;
-        if (mapped_frame(pixel_data->buffer, W, H, nparts, fill)) {
+        const MappedResult mr = g.unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, nparts, fill);
+        if (mr == kMapped) {
             g.pinned_frames++;
             for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
             HIPCHECK(hipSetDevice(g.devs[0]->device));
             return;
         }
-        // the registration no longer maps the caller's pages: pin anew, render the frame by copy
-        drop_registration(pixel_data->buffer, pixel_data->bufferSize);
-        g.stale_pins++;
-        pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        if (mr == kStaleMap) {
+            // the registration no longer maps the caller's pages: pin anew, render the frame by copy
+            drop_registration(pixel_data->buffer, pixel_data->bufferSize);
+            g.stale_pins++;
+            pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
+        } else if (!g.unmapped) {
+            g.unmapped = true;        // a device cannot address the buffer: copy from now on
+            fprintf(stderr, "s3r: a device has no mapping of the caller's buffer; delivering by copy\n");
+        }
     }
     if (copy_bytes) {
         if (pinned && copy_words) stamp_probes(pixel_data->buffer, copy_words);
