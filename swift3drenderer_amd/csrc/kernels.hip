@@ -255,12 +255,12 @@ __device__ unsigned long long g_wgt[kWgTimesMax * kWgSlots];
     for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 4 + i_] = wgc[i_]; \
     g_wgt[blockIdx.x * kWgSlots + 7] = (n); \
     for (int i_ = 0; i_ < 3; i_++) g_wgt[blockIdx.x * kWgSlots + 8 + i_] = wgn[i_]; } } while (0)
-// k_geometry workgroups (slot + row block * grid x): 0 start, 1 slot set up, 2 bins set, 3 last wave done
-constexpr uint32_t kGeoTimesMax = 8192;
+// k_geometry workgroups (slot * 64 + row block): 0 start, 1 slot set up, 2 bins set, 3 last wave done
+constexpr uint32_t kGeoTimesMax = 16384;
 __device__ unsigned long long g_gwt[kGeoTimesMax * 4];
-#define S3R_GWT(k) do { const uint32_t g_ = blockIdx.x + blockIdx.y * gridDim.x; \
+#define S3R_GWT(k) do { const uint32_t g_ = slot * 64u + rb; \
     if (threadIdx.x == 0 && g_ < kGeoTimesMax) g_gwt[g_ * 4 + (k)] = wall_clock64(); } while (0)
-#define S3R_GWT_END() do { const uint32_t g_ = blockIdx.x + blockIdx.y * gridDim.x; \
+#define S3R_GWT_END() do { const uint32_t g_ = slot * 64u + rb; \
     if ((threadIdx.x & 63u) == 0 && g_ < kGeoTimesMax) atomicMax(&g_gwt[g_ * 4 + 3], wall_clock64()); } while (0)
 #else
 #define S3R_GWT(k) do { } while (0)
@@ -543,14 +543,20 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
     float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
-    uint32_t nbins, uint32_t *__restrict__ order) {
+    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb) {
     __shared__ TriSetup sts;
     extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
-    const uint32_t tid = threadIdx.x, slot = blockIdx.x, rb = blockIdx.y;
-    if (slot >= 2u * ntri) {                   // the extra column: this frame's fragment order
-        if (rb == 0) order_bins(order + nbins, nbins, order);
+    // slot-major 1-D grid: workgroup 0 (with `order`) computes this frame's fragment order, then the
+    // row blocks of slot 0, of slot 1, ...  The dispatcher starts workgroups in index order, so a
+    // slot's row blocks start together and the appended clip slots (2T > slot >= T, dead unless
+    // the near plane cut their triangle) come last: a large triangle's long walks start within the
+    // first microsecond instead of after every slot's earlier row blocks.
+    const uint32_t g0 = blockIdx.x;
+    if (order && g0 == 0) {
+        order_bins(order + nbins, nbins, order);
         return;
     }
+    const uint32_t tid = threadIdx.x, gs = g0 - (order ? 1u : 0u), slot = gs / nrb, rb = gs - slot * nrb;
 #ifdef S3R_STATS
     const unsigned long long t_start = wall_clock64();
     if (tid == 0) atomicMin(&g_tstats[2], t_start);
@@ -2159,10 +2165,11 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri + (order ? 1u : 0u), (rows_local + kGeoRows - 1) / kGeoRows),
+    const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
+    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order);
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

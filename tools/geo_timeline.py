@@ -2,7 +2,7 @@
 """Per-workgroup timeline of one k_geometry launch (timing build build/librender_wgt.so, see
 tools/wg_timeline.py; run on the GPU box, ideally with S3R_SERIAL=1).
 
-Each geometry workgroup (slot, block of 128 local rows) stamps the 100 MHz wall clock at its start,
+Each geometry workgroup (slot, block of 128 local rows; record slot * 64 + row block) stamps the 100 MHz wall clock at its start,
 after thread 0 set the slot up, after the bins were set, and when its last wave finished the row /
 segment-start walks.  Prints the launch span and the phase durations of live and dead slots.
 
@@ -47,11 +47,11 @@ def main():
     for _ in range(20):
         r.render_bands(poses.hold(a.pose), W, H, B, N, 0, buf.data_ptr(), st)
     torch.cuda.synchronize()
-    out = (ctypes.c_uint64 * (4 * 8192))()
-    lib.s3r_stats_geo_times(out, 8192)            # clear
+    out = (ctypes.c_uint64 * (4 * 16384))()
+    lib.s3r_stats_geo_times(out, 16384)           # clear
     r.render_bands(poses.hold(a.pose), W, H, B, N, 0, buf.data_ptr(), st)
     torch.cuda.synchronize()
-    n = lib.s3r_stats_geo_times(out, 8192)
+    n = lib.s3r_stats_geo_times(out, 16384)
     t = np.frombuffer(out, dtype=np.uint64)[: 4 * n].reshape(n, 4).astype(np.int64)
     t = t[t[:, 0] > 0]
     t0 = t[:, 0].min()
@@ -68,11 +68,10 @@ def main():
                         ('total', rel[m, 3] - rel[m, 0])]:
             p = np.percentile(v, [10, 50, 90, 100])
             print(f'  {lab} {name:6s} p10 {p[0]:7.2f}  p50 {p[1]:7.2f}  p90 {p[2]:7.2f}  max {p[3]:7.2f} us')
-    nslots = r.scene_counts()[4]
     wt = rel[:, 3] - rel[:, 2]
     for i in np.argsort(-np.where(live, wt, -1))[:6]:
         g = int(idx[i])
-        print(f'  slow walk: slot {g % nslots} row block {g // nslots}: start {rel[i, 0]:.2f} setup {rel[i, 1] - rel[i, 0]:.2f} '
+        print(f'  slow walk: slot {g // 64} row block {g % 64}: start {rel[i, 0]:.2f} setup {rel[i, 1] - rel[i, 0]:.2f} '
               f'walks {wt[i]:.2f} us')
     r.shutdown()
 
