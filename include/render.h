@@ -136,6 +136,16 @@ void s3r_host_stats(uint64_t out[12]);
  * S3R_FILL_THREADS, or 4 (one device) / 8 (several).  Returns 0, or -1 on a bad mode or thread
  * count (0 or > 64).  s3r_delivery() returns the mode in effect (0-3). */
 int s3r_set_delivery(int mode, int fill_threads);
+
+/* Host fill profile since the last call (then cleared), sums over its frames in ns: out[0] frames,
+ * out[1] updateAndRender's entry to the frame's start (t0), then after t0: out[2] device 0's
+ * launches issued, out[3] the devices' finish (stream drained), out[4] the fill threads' finish,
+ * out[5] fill threads joined; out[6] 1 if the fill threads are placed one per CPU domain, out[7]
+ * the NUMA node of the buffer they were placed for (int64, -1 unknown); for fill thread t = 1..n at
+ * out[8 + 4(t - 1)]: the CPU it last ran on,
+ * its summed finish time, the pixels it wrote.  Returns n (<= max_threads); out holds
+ * 8 + 4 * max_threads words. */
+uint32_t s3r_fill_profile(uint64_t *out, uint32_t max_threads);
 int s3r_delivery(void);
 
 /* Rows of a height-row frame owned by `part`. */

@@ -19,13 +19,16 @@
 // devices' HIP calls do not serialise.  The call returns when every part has landed.
 #include <dlfcn.h>
 #include <limits.h>
+#include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -169,13 +172,22 @@ struct HostScene {
 // sleep on a condition variable (a 60 Hz caller does not keep cores busy).
 class Pool {
   public:
-    void start(int workers) {
+    // cpus (optional): worker i runs on the CPUs of cpus[i - 1]
+    void start(int workers, const std::vector<cpu_set_t> *cpus = nullptr) {
         stop();
         stop_.store(false);
         // each worker starts from the generation of now: a run() issued before it is scheduled is
         // still seen as new
         const uint64_t g0 = gen_.load(std::memory_order_acquire);
-        for (int i = 1; i <= workers; i++) th_.emplace_back([this, i, g0] { loop(i, g0); });
+        for (int i = 1; i <= workers; i++) {
+            cpu_set_t set;
+            const bool pin = cpus && (size_t)i <= cpus->size();
+            if (pin) set = (*cpus)[i - 1];
+            th_.emplace_back([this, i, g0, pin, set] {
+                if (pin) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+                loop(i, g0);
+            });
+        }
     }
     void stop() {
         if (th_.empty()) return;
@@ -303,11 +315,18 @@ struct Lib {
     int delivery = -1;
     int fill_threads = -1;                     // host fill threads; -1: S3R_FILL_THREADS or the default
     Pool fill_pool;
+    int fill_node = -2;                        // NUMA node the fill threads were placed for
+    bool fill_placed = false;                  // fill threads pinned one per CPU domain (fill_placement)
     uint64_t copy_frames = 0, direct_frames = 0, fill_frames = 0;
     // adaptive host fill: eighths of the sky bins the GPUs write themselves, and the smoothed
     // (fill threads' finish - devices' finish) in microseconds that steers it
     int fill_gpu = -1;
     double fill_skew_us = 0;
+    // s3r_fill_profile: frames, sums of the devices' / fill threads' finish times (ns after the
+    // frame's start), and per fill thread its last CPU, summed finish time and pixels
+    uint64_t prof_frames = 0, prof_dev_ns = 0, prof_fill_ns = 0, prof_pre_ns = 0, prof_issued_ns = 0, prof_done_ns = 0;
+    std::chrono::steady_clock::time_point call_t0;     // updateAndRender's entry (the profile's pre_ns)
+    struct ThreadProf { int64_t cpu = -1; uint64_t end_ns = 0, px = 0; } prof_thread[65];
     bool unmapped = false;                     // a device could not map a caller buffer: copy only
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
@@ -1124,6 +1143,132 @@ int available_cpus() {
     return n;
 }
 
+// Where the fill threads run.  The fill is streaming stores into the caller's buffer, ~20 GB/s per
+// core; on a chiplet CPU (EPYC: 8 cores per L3 / CCD, one link into the I/O die per CCD) the
+// writes of one CCD share that link, and writes to the other socket's memory cross the socket
+// link.  Unplaced, two fill threads may share a CCD or sit on the far socket, and a frame's fill
+// then takes up to half again as long (measured on the MI355X host, an EPYC 9575F shared with
+// other jobs).  So each fill thread gets a CCD of its own (all that CCD's CPUs: the scheduler picks
+// the core), on the buffer's NUMA node first, least busy CCDs first (/proc/stat over 10 ms).
+// S3R_FILL_PIN=0: no placement.
+struct CpuDomain {
+    std::vector<int> cpus;
+    int node = -1;
+    double busy = 0;
+};
+
+std::vector<int> parse_cpulist(const char *txt) {
+    std::vector<int> out;
+    const char *p = txt;
+    while (*p) {
+        char *e;
+        const long a = strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++) out.push_back((int)c);
+        while (*p == ',' || *p == '\n' || *p == ' ') p++;
+    }
+    return out;
+}
+
+bool read_text(const std::string &path, char *buf, size_t n) {
+    FILE *f = fopen(path.c_str(), "r");
+    if (!f) return false;
+    const size_t k = fread(buf, 1, n - 1, f);
+    fclose(f);
+    buf[k] = 0;
+    return k > 0;
+}
+
+// per-CPU busy jiffies (all fields but idle and iowait) from /proc/stat
+std::vector<uint64_t> cpu_busy() {
+    std::vector<uint64_t> out;
+    FILE *f = fopen("/proc/stat", "r");
+    if (!f) return out;
+    char line[512];
+    while (fgets(line, sizeof line, f)) {
+        if (strncmp(line, "cpu", 3) || line[3] < '0' || line[3] > '9') continue;
+        int cpu;
+        unsigned long long v[8] = {};
+        if (sscanf(line + 3, "%d %llu %llu %llu %llu %llu %llu %llu %llu", &cpu, v, v + 1, v + 2, v + 3, v + 4, v + 5,
+                   v + 6, v + 7) < 5 || cpu < 0 || cpu >= CPU_SETSIZE)
+            continue;
+        if ((size_t)cpu >= out.size()) out.resize(cpu + 1, 0);
+        out[cpu] = v[0] + v[1] + v[2] + v[5] + v[6] + v[7];
+    }
+    fclose(f);
+    return out;
+}
+
+// The process's CPUs grouped by last-level cache, each with its NUMA node (empty: no topology)
+std::vector<CpuDomain> cpu_domains() {
+    std::vector<CpuDomain> doms;
+    cpu_set_t aff;
+    if (sched_getaffinity(0, sizeof aff, &aff) != 0) return doms;
+    std::vector<int> node_of(CPU_SETSIZE, -1);
+    char buf[4096];
+    for (int n = 0; n < 64; n++)
+        if (read_text("/sys/devices/system/node/node" + std::to_string(n) + "/cpulist", buf, sizeof buf))
+            for (int c : parse_cpulist(buf)) node_of[c] = n;
+    std::vector<int> seen(CPU_SETSIZE, 0);
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (!CPU_ISSET(c, &aff) || seen[c]) continue;
+        if (!read_text("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list", buf, sizeof buf))
+            return {};
+        CpuDomain d;
+        for (int x : parse_cpulist(buf))
+            if (x < CPU_SETSIZE && CPU_ISSET(x, &aff) && !seen[x]) {
+                seen[x] = 1;
+                d.cpus.push_back(x);
+            }
+        d.node = node_of[c];
+        if (!d.cpus.empty()) doms.push_back(d);
+    }
+    return doms;
+}
+
+// NUMA node of the page holding p (-1: unknown)
+int page_node(const void *p) {
+    int node = -1;
+    constexpr unsigned long kMpolFNode = 1, kMpolFAddr = 2;
+    if (syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, kMpolFNode | kMpolFAddr) != 0) return -1;
+    return node;
+}
+
+// One CPU set per fill thread (empty: leave the threads to the scheduler)
+std::vector<cpu_set_t> fill_placement(int threads, int node) {
+    std::vector<cpu_set_t> out;
+    const char *e = getenv("S3R_FILL_PIN");
+    if (e && atoi(e) == 0) return out;
+    std::vector<CpuDomain> doms = cpu_domains();
+    if (doms.size() < 2) return out;
+    const std::vector<uint64_t> b0 = cpu_busy();
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    const std::vector<uint64_t> b1 = cpu_busy();
+    for (auto &d : doms) {
+        for (int c : d.cpus)
+            if ((size_t)c < b0.size() && (size_t)c < b1.size()) d.busy += (double)(b1[c] - b0[c]);
+        d.busy /= (double)d.cpus.size();
+    }
+    std::stable_sort(doms.begin(), doms.end(), [&](const CpuDomain &a, const CpuDomain &b) {
+        const bool la = a.node == node, lb = b.node == node;
+        return la != lb ? la : a.busy < b.busy;
+    });
+    for (int t = 0; t < threads; t++) {
+        const CpuDomain &d = doms[(size_t)t % doms.size()];
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        for (int c : d.cpus) CPU_SET(c, &set);
+        out.push_back(set);
+    }
+    return out;
+}
+
 // Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override):
 // by default 4 (one device) or 8, but no more than the CPUs left beside the calling thread and the
 // nparts - 1 device workers.
@@ -1157,6 +1302,10 @@ struct FillJob {
     std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
     std::chrono::steady_clock::time_point t0;
     std::atomic<int64_t> dev_end_ns{0}, fill_end_ns{0};   // latest finish of a device part / a fill thread
+    int64_t issued_ns = 0;                                 // part 0's launches issued
+    int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
+    uint64_t thread_px[65] = {};
+    int thread_cpu[65] = {};
 };
 
 void note_end(const FillJob &job, std::atomic<int64_t> &end) {
@@ -1250,6 +1399,9 @@ void fill_worker(void *arg, int idx) {
     }
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
+    job.thread_px[idx] = px;
+    job.thread_cpu[idx] = sched_getcpu();
+    job.thread_end_ns[idx] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     note_end(job, job.fill_end_ns);
 }
 
@@ -1287,6 +1439,8 @@ void deliver_part_direct(void *arg, int i) {
         hf.probe_dev = i == 0 && hf.flags_dev ? frame_dev : nullptr;
         render_core(d, job.W, job.H, fp.band, fp.nparts, fp.part, fp.rows_local, frame_dev, d.stream, &hf, true);
     }
+    if (i == 0)
+        job.issued_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     HIPCHECK(hipStreamSynchronize(d.stream));
     note_end(job, job.dev_end_ns);
 }
@@ -1320,7 +1474,17 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
         g.fill_gpu = e ? atoi(e) : (int)(2 * (nparts - 1));
         g.fill_gpu = g.fill_gpu < 0 ? 0 : (g.fill_gpu > 8 ? 8 : g.fill_gpu);
     }
-    if (fill && g.fill_pool.workers() != job.threads) g.fill_pool.start(job.threads);
+    if (fill) {
+        // (re)start the fill threads, placed for this buffer's memory node, when the thread count or
+        // the node changes
+        const int node = page_node(buffer);
+        if (g.fill_pool.workers() != job.threads || node != g.fill_node) {
+            const std::vector<cpu_set_t> cpus = fill_placement(job.threads, node);
+            g.fill_pool.start(job.threads, cpus.empty() ? nullptr : &cpus);
+            g.fill_node = node;
+            g.fill_placed = !cpus.empty();
+        }
+    }
     const uint32_t band = nparts == 1 ? H : g.band;
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
@@ -1364,7 +1528,21 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
     job.t0 = std::chrono::steady_clock::now();
     if (fill) g.fill_pool.launch(fill_worker, &job, job.threads + 1);
     g.pool.run(deliver_part_direct, &dd, (int)nparts);
-    if (fill) g.fill_pool.join();
+    if (fill) {
+        g.fill_pool.join();
+        g.prof_frames++;
+        const auto now = std::chrono::steady_clock::now();
+        g.prof_pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(job.t0 - g.call_t0).count();
+        g.prof_issued_ns += (uint64_t)job.issued_ns;
+        g.prof_done_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - job.t0).count();
+        g.prof_dev_ns += (uint64_t)job.dev_end_ns.load();
+        g.prof_fill_ns += (uint64_t)job.fill_end_ns.load();
+        for (int t = 1; t <= job.threads && t <= 64; t++) {
+            g.prof_thread[t].cpu = job.thread_cpu[t];
+            g.prof_thread[t].end_ns += (uint64_t)job.thread_end_ns[t];
+            g.prof_thread[t].px += job.thread_px[t];
+        }
+    }
     if (fill && !getenv("S3R_FILL_GPU")) {
         // one step towards balance between the fill threads and the devices
         const double skew = (double)(job.fill_end_ns.load() - job.dev_end_ns.load()) / 1e3;
@@ -1390,6 +1568,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
 extern "C" {
 
 __attribute__((visibility("default"))) void updateAndRender(const PixelData *pixel_data, const Input *input) {
+    g.call_t0 = std::chrono::steady_clock::now();
     const uint32_t W = pixel_data->width, H = pixel_data->height;
     frame_begin(input, W, H);
     const size_t npx = (size_t)W * H;
@@ -1573,6 +1752,31 @@ __attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[12]) {
     out[11] = g.fill_gpu < 0 ? 0 : (uint64_t)g.fill_gpu;
 }
 
+__attribute__((visibility("default"))) uint32_t s3r_fill_profile(uint64_t *out, uint32_t max_threads) {
+    uint32_t n = 0;
+    for (uint32_t t = 1; t <= 64; t++)
+        if (g.prof_thread[t].cpu >= 0) n = t;
+    n = n < max_threads ? n : max_threads;
+    out[0] = g.prof_frames;
+    out[1] = g.prof_pre_ns;
+    out[2] = g.prof_issued_ns;
+    out[3] = g.prof_dev_ns;
+    out[4] = g.prof_fill_ns;
+    out[5] = g.prof_done_ns;
+    out[6] = g.fill_placed ? 1 : 0;
+    out[7] = (uint64_t)(int64_t)g.fill_node;
+    for (uint32_t t = 1; t <= n; t++) {
+        uint64_t *o = out + 8 + 4 * (t - 1);
+        o[0] = (uint64_t)g.prof_thread[t].cpu;
+        o[1] = g.prof_thread[t].end_ns;
+        o[2] = g.prof_thread[t].px;
+        o[3] = 0;
+    }
+    g.prof_frames = g.prof_dev_ns = g.prof_fill_ns = g.prof_pre_ns = g.prof_issued_ns = g.prof_done_ns = 0;
+    for (auto &t : g.prof_thread) t = Lib::ThreadProf{};
+    return n;
+}
+
 __attribute__((visibility("default"))) int s3r_set_delivery(int mode, int fill_threads) {
     if (mode < -1 || mode > kFill || fill_threads == 0 || fill_threads > 64) return -1;
     g.fill_pool.stop();
@@ -1639,7 +1843,7 @@ __attribute__((visibility("default"))) uint32_t s3r_stats_wg_times(uint64_t *out
     return wg_times_read(reinterpret_cast<unsigned long long *>(out), max_wg);
 }
 
-// Timing build only (-DS3R_WGTIME): per k_geometry workgroup (slot + row block * 2T) of the launches since the
+// Timing build only (-DS3R_WGTIME): per k_geometry workgroup (slot * 64 + row block) of the launches since the
 // last call, 100 MHz wall clock: out[4 * wg + k], k = 0 start, 1 slot set up, 2 bins set, 3 end.  Returns
 // the number of workgroup records copied (0 in the product build) and clears them.
 __attribute__((visibility("default"))) uint32_t s3r_stats_geo_times(uint64_t *out, uint32_t max_wg) {

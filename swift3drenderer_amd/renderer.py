@@ -19,7 +19,8 @@ LIB_PATH = os.environ.get('S3R_LIB') or os.path.join(PKG, 'librender.so')
 EXPORTS = ['updateAndRender', 's3r_configure', 's3r_configure_devices', 's3r_devices', 's3r_shutdown',
            's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host', 's3r_host_pinned', 's3r_host_stats',
            's3r_render_bands', 's3r_bands_to_host', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect',
-           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_delivery', 's3r_delivery']
+           's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_delivery', 's3r_delivery',
+           's3r_fill_profile']
 
 _lib = None
 # host frames of update_and_render(out=None), one per shape, kept for the process: the library may
@@ -72,6 +73,8 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_set_delivery.restype = ctypes.c_int
     lib.s3r_delivery.argtypes = []
     lib.s3r_delivery.restype = ctypes.c_int
+    lib.s3r_fill_profile.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+    lib.s3r_fill_profile.restype = ctypes.c_uint32
     missing = [name for name in EXPORTS if not hasattr(lib, name)]
     if missing:
         raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
@@ -121,6 +124,20 @@ class Renderer:
         keys = ('pinned_frames', 'pageable_frames', 'registrations', 'merges', 'held', 'stale', 'copy_frames',
                 'direct_frames', 'fill_frames', 'fill_threads', 'link_bytes', 'fill_gpu_eighths')
         return dict(zip(keys, (int(v) for v in out)))
+
+    def fill_profile(self) -> dict:
+        """Host fill profile since the last call (include/render.h s3r_fill_profile), means per frame in
+        us: entry to frame start (pre), then after the start: launches issued, devices drained, fill
+        threads done, joined; per thread its CPU, mean finish and pixels per frame."""
+        out = (ctypes.c_uint64 * (8 + 4 * 64))()
+        n = self.lib.s3r_fill_profile(out, 64)
+        f = max(int(out[0]), 1)
+        us = lambda v: round(v / f / 1e3, 1)
+        return {'frames': int(out[0]), 'pre_us': us(out[1]), 'issued_us': us(out[2]), 'dev_end_us': us(out[3]),
+                'fill_end_us': us(out[4]), 'joined_us': us(out[5]), 'placed': bool(out[6]),
+                'node': ctypes.c_int64(out[7]).value,
+                'threads': [{'cpu': int(out[8 + 4 * t]), 'end_us': us(out[9 + 4 * t]), 'px': int(out[10 + 4 * t] // f)}
+                            for t in range(n)]}
 
     DELIVERIES = {'env': -1, 'auto': 0, 'copy': 1, 'direct': 2, 'fill': 3}
 

@@ -210,3 +210,37 @@ def test_host_fill_split_matches_oracle(multi, scene_dir, monkeypatch, split, de
         assert st['fill_gpu_eighths'] == split and st['fill_frames'] == 3, st
     finally:
         multi.set_delivery('env')
+
+
+def l3_domains():
+    """CPU -> last-level-cache domain id, from sysfs (empty where the topology is not exposed)."""
+    import glob
+    dom = {}
+    for path in glob.glob('/sys/devices/system/cpu/cpu[0-9]*/cache/index3/shared_cpu_list'):
+        cpu = int(path.split('/cpu/cpu')[1].split('/')[0])
+        dom[cpu] = open(path).read().strip()
+    return dom
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('pin', ['1', '0'])
+def test_host_fill_thread_placement(multi, scene_dir, monkeypatch, pin):
+    """Host fill threads placed one per CPU domain (render_api.cpp fill_placement): frames still match
+    the oracle, the profile reports the placement and the buffer's node, and the threads' last CPUs lie
+    in distinct last-level-cache domains; S3R_FILL_PIN=0 leaves them to the scheduler."""
+    monkeypatch.setenv('S3R_FILL_PIN', pin)
+    multi.set_delivery('fill', 4)            # (restarts the fill threads: placement is redone)
+    try:
+        multi.fill_profile()
+        frames_vs_oracle(multi, scene_dir['full'], pose_frames('P_over', 1920, 1080, extra=4), [0])
+        prof = multi.fill_profile()
+        assert prof['frames'] >= 5 and len(prof['threads']) == 4, prof
+        assert sum(t['px'] for t in prof['threads']) > 0
+        dom = l3_domains()
+        if pin == '0':
+            assert not prof['placed'], prof
+        elif len(set(dom.values())) >= 4:
+            assert prof['placed'], prof
+            assert len({dom[t['cpu']] for t in prof['threads']}) == 4, (prof, dom)
+    finally:
+        multi.set_delivery('env')

@@ -85,12 +85,14 @@ def main():
     refs = [ctypes.byref(h) for h in buf.halves]
     for k in range(a.warmup):
         r.lib.updateAndRender(refs[k & 1], hr)
+    r.fill_profile()                                  # clear
     per = np.empty(a.frames)
     for k in range(a.frames):
         t0 = time.perf_counter()
         r.lib.updateAndRender(refs[k & 1], hr)
         per[k] = time.perf_counter() - t0
     st = r.host_stats()
+    st['fill_profile'] = r.fill_profile()
     st.update(numa_report(buf))
     print(json.dumps({'delivery': a.delivery, 'devices': devs, 'median_ms': round(float(np.median(per)) * 1e3, 4),
                       'p10_ms': round(float(np.percentile(per, 10)) * 1e3, 4),
