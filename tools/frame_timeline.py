@@ -33,6 +33,7 @@ def main():
     ap.add_argument('--height', type=int, default=2160)
     ap.add_argument('--delivery', default='fill')
     ap.add_argument('--frames', type=int, default=20)
+    ap.add_argument('--dump', default=None, help='save the last frame\'s workgroup records (.npz)')
     a = ap.parse_args()
     os.environ.setdefault('S3R_LIB', os.path.join(ROOT, 'build', 'librender_wgt.so'))
     from bench import DoubleBuffer
@@ -71,6 +72,8 @@ def main():
         g0, g1 = g[:, 0].min(), g[:, 3].max()
         f0, f1 = fr[:, 0].min(), fr[:, 3].max()
         rows.append([call, (g1 - g0) * 0.01, (f0 - g1) * 0.01, (f1 - f0) * 0.01, call - (f1 - g0) * 0.01])
+    if a.dump:
+        np.savez(a.dump, geo=g, frag=fr)
     v = np.array(rows)
     med = np.median(v, axis=0)
     out = {'delivery': a.delivery, 'frames': a.frames, 'call_us': round(med[0], 1), 'geometry_span_us': round(med[1], 1),

@@ -38,6 +38,35 @@ __global__ void __launch_bounds__(256) k_bins(unsigned *frame, const unsigned *l
     }
 }
 
+// the fragment kernel's store pattern: per covered bin, each wave (row) stores its six 64-px chunks
+// one 256-B wave store at a time, ~20 % of the chunks skipped (all background: the host fills them);
+// ROT: each store shifted to the 64-B line grid (the wave stores pixels [cx0 - r, cx0 - r + 64), r =
+// the chunk start's pixel offset inside its line: the previous chunk's last r pixels carried over in
+// lanes < r by a lane rotation), so every store covers whole lines
+template <bool ROT>
+__global__ void __launch_bounds__(256) k_chunks(unsigned *frame, const unsigned *list, unsigned v) {
+    const unsigned b = list[blockIdx.x];
+    const unsigned wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned y = (b / SEGS) * BIN_H + wave, xs = (b % SEGS) * BIN_W;
+    unsigned *row = frame + (size_t)y * W;
+    const unsigned r = ROT ? (unsigned)(((uintptr_t)(row + xs) >> 2) & 15u) : 0u;
+    unsigned carry = 0xFFFFFFFFu;
+    for (unsigned q = 0; q < BIN_W / 64; q++) {
+        const bool covered = ((b * 7u + q * 13u + wave) * 2654435761u >> 20) % 10u >= 2u;
+        const unsigned cx0 = xs + 64u * q;
+        const unsigned px = covered ? (v + cx0 + lane) & 0xFFFFFFu : 0xFFFFFFFFu;
+        if (!ROT) {
+            if (covered) row[cx0 + lane] = px;
+            continue;
+        }
+        const unsigned rot = (unsigned)__shfl((int)px, (int)((lane - r) & 63u));
+        const unsigned val = lane >= r ? rot : carry;
+        if (val != 0xFFFFFFFFu) row[cx0 - r + lane] = val;
+        carry = rot;
+    }
+    if (ROT && lane < r && carry != 0xFFFFFFFFu) row[xs + BIN_W - r + lane] = carry;
+}
+
 // contiguous: one workgroup per 6 KiB (a bin's bytes), 4 B per lane
 __global__ void __launch_bounds__(256) k_flat(unsigned *dst, unsigned n, unsigned v) {
     const size_t base = (size_t)blockIdx.x * 1536;
@@ -108,6 +137,30 @@ int main() {
             Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<1, false>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
         report("kernel bins 4B/lane nontemporal", time_it(s, e0, e1, [](hipStream_t st, void *p) {
             Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<1, true>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
+        report("kernel chunks (fragment pattern)", time_it(s, e0, e1, [](hipStream_t st, void *p) {
+            Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_chunks<false>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered * 8 / 10);
+        report("kernel chunks line-aligned (rotated)", time_it(s, e0, e1, [](hipStream_t st, void *p) {
+            Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_chunks<true>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered * 8 / 10);
+        for (int rot = 0; rot < 2; rot++) {      // both chunk kernels write exactly the covered chunks
+            memset(host, 0, fb);
+            if (rot) hipLaunchKernelGGL((k_chunks<true>), dim3(c.nbins), dim3(256), 0, s, c.host_dev, c.list, 7u);
+            else hipLaunchKernelGGL((k_chunks<false>), dim3(c.nbins), dim3(256), 0, s, c.host_dev, c.list, 7u);
+            CK(hipStreamSynchronize(s));
+            size_t bad = 0;
+            for (unsigned i = 0; i < nb; i++) {
+                const unsigned b = hlist[i];
+                for (unsigned wv = 0; wv < BIN_H; wv++)
+                    for (unsigned q = 0; q < BIN_W / 64; q++) {
+                        const bool cov = ((b * 7u + q * 13u + wv) * 2654435761u >> 20) % 10u >= 2u;
+                        const unsigned y = (b / SEGS) * BIN_H + wv;
+                        for (unsigned l = 0; l < 64; l++) {
+                            const unsigned x = (b % SEGS) * BIN_W + 64 * q + l;
+                            bad += host[(size_t)y * W + x] != (cov ? ((7u + x) & 0xFFFFFFu) : 0u);
+                        }
+                    }
+            }
+            printf("  chunks %s: %zu wrong pixels\n", rot ? "rotated" : "plain", bad);
+        }
         {   // (row segments are 16-B aligned in every mode)
             report("kernel bins 16B/lane", time_it(s, e0, e1, [](hipStream_t st, void *p) {
                 Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<4, false>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);

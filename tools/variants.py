@@ -39,7 +39,7 @@ def run():
                    S3R_SERIAL=os.environ.get('S3R_SERIAL', '1'))
         d = os.path.join(out_root, tag)
         cmd = ['rocprofv3', '--kernel-trace', '--stats', '-d', d, '-o', 'run', '--output-format', 'csv', '--',
-               sys.executable, 'bench.py', '--steps', '10', '--warmup', '2', '--no-cpu-baseline', '--no-e2e'] + extra
+               sys.executable, 'bench.py', '--steps', '10', '--warmup', '2', '--no-cpu-baseline'] + extra
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
         line = [l for l in r.stdout.splitlines() if l.startswith('{')]
         fps = line[-1].split('"value": ')[1].split(',')[0] if line else '?'
