@@ -514,6 +514,51 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
     }
 }
 
+// Host fill: the bins' sky flags, published from inside k_geometry by one extra workgroup (dispatched
+// before the geometry workgroups) as soon as every geometry workgroup has reserved its pairs: each
+// counts itself, once its bin phase is over (or at once for a dead slot), in its row block's counter
+// (geo_cnt[rb * kGeoCntStride], own cache line: 2T arrivals each instead of all on one address); the
+// publisher spins until every row block has its 2T, reads the final counts with device-scope
+// (L2-bypassing) loads -- every bincnt atomicAdd of a workgroup returned before its barrier and its
+// arrival was issued after it -- and stores flags[b] = tag, | kSkyBit for a bin no slot meets (the
+// host fills it), | kGpuBit instead for sky bins with b % 8 < gpu_eighths (the fragment kernel writes
+// their background).  probe: pixel 0 of the caller's buffer, set to kMapProbe through the mapping
+// before flags[0] is published (the host's stale-mapping check).  It then resets the counters for
+// the buffer set's next frame (no arrival is left: each row block had all of its 2T).
+constexpr uint32_t kGeoCntStride = 16;           // uint32 words: one 64-B line per row block
+constexpr uint32_t kGeoCntMax = 256;             // row blocks with a counter (more: k_sky_flags)
+static_assert(kGeoCntMax * kGeoCntStride == kGeoCounterWords, "geometry counters: s3r_kernels.h's size");
+struct SkyFlags {
+    uint32_t *flags;                  // null: no host fill
+    uint32_t *probe;
+    uint32_t *geo_cnt;
+    uint32_t tag, gpu_eighths;
+};
+
+__device__ void publish_sky_flags(const SkyFlags &sf, const uint32_t *__restrict__ bincnt, uint32_t nbins,
+                                  uint32_t nrb, uint32_t arrivals) {
+    for (uint32_t r = threadIdx.x; r < nrb; r += blockDim.x)
+        while (__hip_atomic_load(sf.geo_cnt + r * kGeoCntStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < arrivals)
+            __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) {
+        const uint32_t c = __hip_atomic_load(bincnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t f = c != 0u ? sf.tag : ((b & 7u) < sf.gpu_eighths ? (sf.tag | kGpuBit) : (sf.tag | kSkyBit));
+        if (b == 0 && sf.probe) {
+            __hip_atomic_store(sf.probe, kMapProbe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(sf.flags, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            __hip_atomic_store(sf.flags + b, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    for (uint32_t r = threadIdx.x; r < nrb; r += blockDim.x)
+        __hip_atomic_store(sf.geo_cnt + r * kGeoCntStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void geo_arrive(const SkyFlags &sf, uint32_t rb) {
+    if (sf.flags && threadIdx.x == 0) atomicAdd(sf.geo_cnt + rb * kGeoCntStride, 1u);
+}
+
 // ------------------------------------------------------------------ K1: geometry, one launch
 // Per frame, on the geometry stream (overlapping the previous frame's fragment kernel): one
 // workgroup per (slot, block of kGeoRows local rows) x 3 components.
@@ -543,7 +588,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
     float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
-    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb) {
+    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky) {
     __shared__ TriSetup sts;
     extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
     // slot-major 1-D grid: workgroup 0 (with `order`) computes this frame's fragment order, then the
@@ -556,7 +601,12 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
         order_bins(order + nbins, nbins, order);
         return;
     }
-    const uint32_t tid = threadIdx.x, gs = g0 - (order ? 1u : 0u), slot = gs / nrb, rb = gs - slot * nrb;
+    const uint32_t first = (order ? 1u : 0u) + (sky.flags ? 1u : 0u);    // the geometry workgroups' first index
+    if (sky.flags && g0 == first - 1u) {
+        publish_sky_flags(sky, bincnt, nbins, nrb, 2u * ntri);
+        return;
+    }
+    const uint32_t tid = threadIdx.x, gs = g0 - first, slot = gs / nrb, rb = gs - slot * nrb;
 #ifdef S3R_STATS
     const unsigned long long t_start = wall_clock64();
     if (tid == 0) atomicMin(&g_tstats[2], t_start);
@@ -573,7 +623,11 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     }
     __syncthreads();
     S3R_GWT(1);
-    if (sts.kind == kDead) { S3R_GWT_END(); return; }
+    if (sts.kind == kDead) {
+        geo_arrive(sky, rb);
+        S3R_GWT_END();
+        return;
+    }
     const uint32_t xmin = sts.xmin, xmax = sts.xmax, ymin = sts.ymin, ymax = sts.ymax;
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
 
@@ -619,6 +673,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
         }
     }
     __syncthreads();
+    geo_arrive(sky, rb);
     S3R_GWT(2);
 
     // exact row and start-table points: lane (row, component) walks the reference's sequence exactly
@@ -2157,19 +2212,34 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order) {
-    if (ntri == 0 || rows_local == 0) {
-        if (done) (void)hipEventRecord(done, st);
+                     uint32_t *order, const GeoSkyFlags *gsf) {
+    const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
+    if (ntri == 0 || rows_local == 0 || (gsf && nrb > kGeoCntMax)) {
+        // nothing to set up (every bin is sky), or more row blocks than counters: k_sky_flags publishes
+        if (ntri && rows_local) {
+            const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
+            hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
+                                  st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
+                                  nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
+                                  (uint32_t)fragment_bins(W, rows_local), order, nrb,
+                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u});
+        }
+        if (gsf)
+            launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
+                             st, done);
+        else if (done)
+            (void)hipEventRecord(done, st);
         return;
     }
+    const SkyFlags sky = gsf ? SkyFlags{gsf->flags, gsf->probe, gsf->geo_cnt, gsf->tag, gsf->gpu_eighths}
+                             : SkyFlags{nullptr, nullptr, nullptr, 0u, 0u};
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
-    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)),
+    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? 1u : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb);
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

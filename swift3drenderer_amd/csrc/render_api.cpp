@@ -135,6 +135,7 @@ struct Dev {
     // (either path)
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
+    uint32_t *geo_cnt = nullptr;             // host fill: per buffer set, k_geometry's bin-phase count
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
     // the previous frame's stream; NULL is a valid caller stream (the legacy default stream), so
     // whether a previous frame exists is its own flag
@@ -566,7 +567,7 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv};
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv, d.geo_cnt};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
@@ -905,14 +906,21 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     d.hp.lap(2);
     const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
+    // host fill: the geometry launch also publishes the bins' sky flags, as soon as every workgroup's
+    // pair reservations are in (one extra workgroup waits for them on per-row-block counters)
+    GeoSkyFlags gsf{};
+    if (hf && hf->flags_dev) {
+        if (!d.geo_cnt) {
+            d.geo_cnt = dalloc<uint32_t>((size_t)kSets * kGeoCounterWords);
+            HIPCHECK(hipMemset(d.geo_cnt, 0, (size_t)kSets * kGeoCounterWords * sizeof(uint32_t)));
+            HIPCHECK(hipDeviceSynchronize());      // (null-stream memset: finish before the geometry stream)
+        }
+        gsf = GeoSkyFlags{hf->flags_dev, hf->probe_dev, d.geo_cnt + (size_t)p * kGeoCounterWords, hf->tag,
+                          hf->gpu_eighths};
+    }
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
-                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo,
-                    chained || (hf && hf->flags_dev) ? nullptr : d.geo_done[p], lpt ? d.order[p] : nullptr);
-    // host fill: the bins' sky flags to the host as soon as the counts are final (before the
-    // fragment kernel, which resets the counts, may start)
-    if (hf && hf->flags_dev)
-        launch_sky_flags(d.bincnt[p], nbins, hf->flags_dev, hf->tag, hf->probe_dev, hf->gpu_eighths, geo,
-                         chained ? nullptr : d.geo_done[p]);
+                    rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
+                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event

@@ -40,11 +40,19 @@ uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
 // headers and pairs, and rowtab (2T x rows_local x start_entries(W) x float4): exact barycentrics of
 // every live slot's bbox rows at x = xmin and at each 384-pixel boundary inside the bbox.
 uint32_t start_entries(uint32_t W);
+// Host fill (render_api.cpp): with gsf the launch also publishes the bins' sky flags as soon as every
+// workgroup's pair reservations are in (see launch_sky_flags for flags / tag / probe / gpu_eighths);
+// geo_cnt: kGeoCounterWords zeroed device words (the launch leaves them 0), one set per launch in flight.
+constexpr uint32_t kGeoCounterWords = 256 * 16;
+struct GeoSkyFlags {
+    uint32_t *flags, *probe, *geo_cnt;
+    uint32_t tag, gpu_eighths;
+};
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order);
+                     uint32_t *order, const GeoSkyFlags *gsf = nullptr);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
