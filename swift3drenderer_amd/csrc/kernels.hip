@@ -322,6 +322,10 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #ifndef S3R_TWO_PIECE
 #define S3R_TWO_PIECE 1                // batch 0: chunks crossing one binade edge as two linear pieces
 #endif
+#ifndef S3R_LINE_STORES
+#define S3R_LINE_STORES 1              // HOSTW: wave stores on the caller buffer's 64-B line grid
+#endif
+constexpr uint32_t kNoPixel = 0xFFFFFFFFu;   // no store (pixels are 0x00RRGGBB)
 constexpr uint32_t kPX = S3R_PX;       // pixels per lane: a chunk is 64 * kPX consecutive pixels of a row
 constexpr uint32_t kChunk = 64u * kPX;
 constexpr uint32_t kStateBatches = S3R_STATE_BATCHES;  // batches whose walk state persists in LDS
@@ -1162,10 +1166,32 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 
     uint32_t *row = out + orow;
     uint32_t bgm = 0;                    // host fill: this row's chunks no triangle covers (bit q)
+    // HOSTW: the wave's stores on the 64-B line grid of the caller's buffer.  A buffer from glibc's
+    // malloc starts 16 B into a line, so a 64-pixel chunk store would touch five lines, two of them
+    // partly; instead the wave stores the 64 pixels [cx0 - rsh, cx0 - rsh + 64), rsh = the pixel
+    // offset of the row segment's start inside its line: lanes >= rsh this chunk's first 64 - rsh
+    // pixels (a lane rotation), lanes < rsh the previous chunk's last rsh (carried), and after the
+    // last chunk the carried pixels alone.  Every pixel is stored once, by its own workgroup; a
+    // lane with nothing to store (outside the frame, a chunk left to the host fill) holds kNoPixel.
+    // Over an uncached registration (render_api.cpp host_pinned) the link then carries whole lines:
+    // 54.0 instead of 49.1 GB/s for this pattern (tools/micro/pcie_write.hip).
+    const uint32_t rsh = (HOSTW && S3R_LINE_STORES) ? (uint32_t)(((uintptr_t)(row + xs) >> 2) & 15u) : 0u;
+    uint32_t carry = kNoPixel, cx_next = xs;
+    auto put = [&](uint32_t c0x, uint32_t v) {      // the lane's pixel c0x + lane, or kNoPixel
+        if (rsh == 0u) {
+            if (v != kNoPixel) row[c0x + lane] = v;
+            return;
+        }
+        const uint32_t rot = (uint32_t)__shfl((int)v, (int)((lane - rsh) & 63u));
+        const uint32_t o = lane >= rsh ? rot : carry;
+        if (o != kNoPixel) row[c0x - rsh + lane] = o;
+        carry = rot;
+    };
     S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + kChunk * q;
         if (cx0 > xe) break;
+        cx_next = cx0 + kChunk;
         const uint32_t cx1 = min(cx0 + kChunk - 1u, xe);
         const uint32_t x = cx0 + lane;                     // this lane's pixels: x + 64 p, p < kPX
         float depth[kPX], bw0[kPX], bw1[kPX], bw2[kPX];
@@ -1317,6 +1343,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
             for (uint32_t p = 0; p < kPX; p++) any |= row_ok && x + 64u * p <= xe && win[p] >= 0;
             if (__ballot(any) == 0) {
                 if (row_ok) bgm |= 1u << q;
+#pragma unroll
+                for (uint32_t p = 0; p < kPX; p++) put(cx0 + 64u * p, kNoPixel);
                 continue;
             }
         }
@@ -1336,8 +1364,11 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #else
             if (!WF) {
-                if (row_ok && xp <= xe)
-                    row[xp] = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+                const bool act = row_ok && xp <= xe;
+                uint32_t px = kNoPixel;
+                if (act) px = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
+                if (HOSTW) put(cx0 + 64u * p, px);
+                else if (act) row[xp] = px;
             } else {
                 // waterfall over the wave's distinct winners (usually one: a chunk inside one
                 // triangle): each round shades the lanes of one winner, whose record address is
@@ -1361,13 +1392,15 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                         px = shade_core_flat(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
                                              depth[p], tex, ntex);
                 }
-                if (act) row[xp] = px;
+                if (HOSTW) put(cx0 + 64u * p, act ? px : kNoPixel);
+                else if (act) row[xp] = px;
             }
 #endif
 #endif
         }
         S3R_WGC_ADD(2);
     }
+    if (HOSTW && rsh != 0u && lane < rsh && carry != kNoPixel) row[cx_next - rsh + lane] = carry;
     if (HOSTW && host_fill) {
         // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q)
         if (lane == 0) sh.bgm[wave] = bgm;

@@ -990,8 +990,18 @@ bool host_pinned(void *p, size_t n) {
         g.merges++;
     }
     if (g.regs.size() >= 4) unregister_all();
-    // mapped: the host-fill delivery has the GPU write covered bins straight into these pages
-    const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;
+    // mapped: the host-fill delivery has the GPU write covered bins straight into these pages;
+    // uncached (the extended fine-grained pool): with the fragment kernel's line-grid stores the
+    // link then carries whole 64-B lines (54.0 vs 52.0 GB/s for a malloc + 16-B buffer,
+    // tools/micro/pcie_write.hip); S3R_HOST_UNCACHED=0 registers it as before.  A runtime that
+    // refuses the flag gets the plain registration.
+    static const bool uncached = !getenv("S3R_HOST_UNCACHED") || atoi(getenv("S3R_HOST_UNCACHED")) != 0;
+    bool ok = uncached && hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped |
+                                                                hipExtHostRegisterUncached) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;
+    }
     if (!ok) (void)hipGetLastError();
     else g.registrations++;
     g.regs.push_back({a, b, ok});

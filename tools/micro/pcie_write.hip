@@ -107,21 +107,24 @@ int main() {
     CK(hipEventCreate(&e1));
     const size_t fb = (size_t)W * H * 4;
 
-    for (int mode = 0; mode < 3; mode++) {
-        // 0: malloc + register, base +16 B (glibc's large malloc); 1: same, 64-B aligned; 2: hipHostMalloc
+    for (int mode = 0; mode < 5; mode++) {
+        // 0: malloc + register, base +16 B (glibc's large malloc); 1: same, 64-B aligned; 2: hipHostMalloc;
+        // 3: as 0, registered uncached (extended fine-grained); 4: as 0, registered coarse-grained
         void *raw = nullptr;
         unsigned *host = nullptr;
-        if (mode < 2) {
+        if (mode != 2) {
             raw = malloc(fb + 4096);
-            host = (unsigned *)(((uintptr_t)raw + 4095) & ~(uintptr_t)4095) + (mode == 0 ? 4 : 0);
-            CK(hipHostRegister(host, fb, hipHostRegisterPortable | hipHostRegisterMapped));
+            host = (unsigned *)(((uintptr_t)raw + 4095) & ~(uintptr_t)4095) + (mode == 1 ? 0 : 4);
+            const unsigned extra = mode == 3 ? hipExtHostRegisterUncached : (mode == 4 ? hipExtHostRegisterCoarseGrained : 0u);
+            CK(hipHostRegister(host, fb, hipHostRegisterPortable | hipHostRegisterMapped | extra));
         } else {
             CK(hipHostMalloc((void **)&host, fb, hipHostMallocMapped));
         }
         memset(host, 0, fb);
         c.host = host;
         CK(hipHostGetDevicePointer((void **)&c.host_dev, host, 0));
-        const char *name[] = {"malloc+register +16B", "malloc+register aligned", "hipHostMalloc"};
+        const char *name[] = {"malloc+register +16B", "malloc+register aligned", "hipHostMalloc",
+                              "malloc+register +16B uncached", "malloc+register +16B coarse-grained"};
         printf("== %s\n", name[mode]);
         auto report = [&](const char *what, float ms, size_t bytes) {
             printf("  %-34s %8.1f us  %6.1f GB/s\n", what, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
@@ -167,7 +170,7 @@ int main() {
             report("kernel bins 16B/lane nontemporal", time_it(s, e0, e1, [](hipStream_t st, void *p) {
                 Ctx &q = *(Ctx *)p; hipLaunchKernelGGL((k_bins<4, true>), dim3(q.nbins), dim3(256), 0, st, q.host_dev, q.list, 7u); }, &c, 20), covered);
         }
-        if (mode < 2) { CK(hipHostUnregister(host)); free(raw); }
+        if (mode != 2) { CK(hipHostUnregister(host)); free(raw); }
         else CK(hipHostFree(host));
     }
     return 0;
