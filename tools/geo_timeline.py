@@ -31,7 +31,7 @@ def main():
     a = ap.parse_args()
     import torch
     from swift3drenderer_amd import poses, renderer, scene
-    lib = renderer.load_library(os.path.join(ROOT, 'build', 'librender_wgt.so'))
+    lib = renderer.load_library(os.environ.get('S3R_LIB') or os.path.join(ROOT, 'build', 'librender_wgt.so'))
     lib.s3r_stats_geo_times.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     lib.s3r_stats_geo_times.restype = ctypes.c_uint32
     d = tempfile.mkdtemp()
