@@ -459,9 +459,11 @@ __device__ void build_list(const TriSetup *__restrict__ tris, uint32_t nslots, u
 // remaining < kStartPx pixels themselves (a few exact_walk iterations), so the geometry's serial
 // chain does not grow with the number of fragment segments.
 constexpr uint32_t kStartPx = 384;
-__device__ __forceinline__ uint32_t start_index(uint32_t xmin, uint32_t xs, uint32_t *k) {
+// row_starts: the launch's geometry tabulated the row starts only (delivered frames, below): every
+// walk starts at x = xmin.
+__device__ __forceinline__ uint32_t start_index(uint32_t xmin, uint32_t xs, uint32_t *k, bool row_starts = false) {
     const uint32_t jb = xs / kStartPx;
-    if (xs <= xmin || jb * kStartPx <= xmin) { *k = xmin; return 0u; }
+    if (row_starts || xs <= xmin || jb * kStartPx <= xmin) { *k = xmin; return 0u; }
     *k = jb * kStartPx;
     return 1u + jb;
 }
@@ -518,17 +520,17 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
     }
 }
 
-// Host fill: the bins' sky flags, published from inside k_geometry by one extra workgroup (dispatched
-// before the geometry workgroups) as soon as every geometry workgroup has reserved its pairs: each
-// counts itself, once its bin phase is over (or at once for a dead slot), in its row block's counter
-// (geo_cnt[rb * kGeoCntStride], own cache line: 2T arrivals each instead of all on one address); the
-// publisher spins until every row block has its 2T, reads the final counts with device-scope
-// (L2-bypassing) loads -- every bincnt atomicAdd of a workgroup returned before its barrier and its
-// arrival was issued after it -- and stores flags[b] = tag, | kSkyBit for a bin no slot meets (the
-// host fills it), | kGpuBit instead for sky bins with b % 8 < gpu_eighths (the fragment kernel writes
-// their background).  probe: pixel 0 of the caller's buffer, set to kMapProbe through the mapping
-// before flags[0] is published (the host's stale-mapping check).  It then resets the counters for
-// the buffer set's next frame (no arrival is left: each row block had all of its 2T).
+// Host fill: the bins' sky flags, published from inside k_geometry, one extra workgroup per row block
+// of kGeoRows local rows (dispatched before the geometry workgroups): every geometry workgroup counts
+// itself, once its bin phase is over (or at once for a dead slot), in its row block's counter
+// (geo_cnt[rb * kGeoCntStride], own cache line); the row block's publisher spins until its 2T
+// arrivals are in, reads the final counts of the row block's bins with device-scope (L2-bypassing)
+// loads -- every bincnt atomicAdd of a workgroup returned before its barrier and its arrival was
+// issued after it -- and stores flags[b] = tag, | kSkyBit for a bin no slot meets (the host fills
+// it), | kGpuBit instead for sky bins with b % 8 < gpu_eighths (the fragment kernel writes their
+// background).  probe: pixel 0 of the caller's buffer, set to kMapProbe through the mapping before
+// flags[0] is published (the host's stale-mapping check).  Each publisher then resets its counter
+// for the buffer set's next frame (no arrival is left: its row block had all of its 2T).
 constexpr uint32_t kGeoCntStride = 16;           // uint32 words: one 64-B line per row block
 constexpr uint32_t kGeoCntMax = 256;             // row blocks with a counter (more: k_sky_flags)
 static_assert(kGeoCntMax * kGeoCntStride == kGeoCounterWords, "geometry counters: s3r_kernels.h's size");
@@ -539,24 +541,41 @@ struct SkyFlags {
     uint32_t tag, gpu_eighths;
 };
 
+// the row block rb's bins: [rb * rb_bins, (rb + 1) * rb_bins), rb_bins = its fragment row blocks x segs
 __device__ void publish_sky_flags(const SkyFlags &sf, const uint32_t *__restrict__ bincnt, uint32_t nbins,
-                                  uint32_t nrb, uint32_t arrivals) {
-    for (uint32_t r = threadIdx.x; r < nrb; r += blockDim.x)
-        while (__hip_atomic_load(sf.geo_cnt + r * kGeoCntStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < arrivals)
-            __builtin_amdgcn_s_sleep(2);
+                                  uint32_t rb_bins, uint32_t rb, uint32_t arrivals) {
+    uint32_t *cnt = sf.geo_cnt + rb * kGeoCntStride;
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < arrivals) __builtin_amdgcn_s_sleep(2);
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) {
-        const uint32_t c = __hip_atomic_load(bincnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t f = c != 0u ? sf.tag : ((b & 7u) < sf.gpu_eighths ? (sf.tag | kGpuBit) : (sf.tag | kSkyBit));
-        if (b == 0 && sf.probe) {
-            __hip_atomic_store(sf.probe, kMapProbe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(sf.flags, f, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-            __hip_atomic_store(sf.flags + b, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t b0 = rb * rb_bins, b1 = min(nbins, b0 + rb_bins);
+    // kPubUnroll counts per thread in flight at once (the loads go to memory: one round trip each)
+    constexpr uint32_t kPubUnroll = 4;
+    for (uint32_t base = b0; base < b1; base += kPubUnroll * blockDim.x) {
+        uint32_t cs[kPubUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kPubUnroll; u++) {
+            const uint32_t b = base + u * blockDim.x + threadIdx.x;
+            cs[u] = b < b1 ? __hip_atomic_load(bincnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kPubUnroll; u++) {
+            const uint32_t b = base + u * blockDim.x + threadIdx.x;
+            if (b >= b1) break;
+            const uint32_t f = cs[u] != 0u ? sf.tag : ((b & 7u) < sf.gpu_eighths ? (sf.tag | kGpuBit) : (sf.tag | kSkyBit));
+            if (b == 0 && sf.probe) {
+                // the probe reaches the caller's page before flag 0 does: both are stores over the link
+                // from this thread, the second issued once the first completed (rather than a
+                // system-scope release, which would first write back the whole L2)
+                __hip_atomic_store(sf.probe, kMapProbe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_s_waitcnt(0);
+                __hip_atomic_store(sf.flags, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                __hip_atomic_store(sf.flags + b, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
-    for (uint32_t r = threadIdx.x; r < nrb; r += blockDim.x)
-        __hip_atomic_store(sf.geo_cnt + r * kGeoCntStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void geo_arrive(const SkyFlags &sf, uint32_t rb) {
@@ -592,7 +611,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
     float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
-    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky) {
+    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky, uint32_t row_starts) {
     __shared__ TriSetup sts;
     extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
     // slot-major 1-D grid: workgroup 0 (with `order`) computes this frame's fragment order, then the
@@ -605,9 +624,9 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
         order_bins(order + nbins, nbins, order);
         return;
     }
-    const uint32_t first = (order ? 1u : 0u) + (sky.flags ? 1u : 0u);    // the geometry workgroups' first index
-    if (sky.flags && g0 == first - 1u) {
-        publish_sky_flags(sky, bincnt, nbins, nrb, 2u * ntri);
+    const uint32_t pub0 = order ? 1u : 0u, first = pub0 + (sky.flags ? nrb : 0u);   // publishers, geometry
+    if (sky.flags && g0 < first) {
+        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, 2u * ntri);
         return;
     }
     const uint32_t tid = threadIdx.x, gs = g0 - first, slot = gs / nrb, rb = gs - slot * nrb;
@@ -711,7 +730,16 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
 #endif
     row[0] = v;
     // segments starting at or before the first start-table boundary past xmin walk from the row start
+    // -- with row_starts, every segment of the bbox does: the fragment workgroups walk along the row
+    // themselves, off this kernel's critical path (delivered frames: the fragment kernel is bound by
+    // the host link, so its workgroups have the time; the serial boundary walks here were ~15 us of
+    // the launch's ~24)
     const uint32_t sg_xmin = xmin / segw, b1 = (xmin / kStartPx + 1u) * kStartPx;
+    if (row_starts) {
+        to_pairs(sg_xmin, (xmax / segw) + 1u, v);
+        S3R_GWT_END();
+        return;
+    }
     to_pairs(sg_xmin, min((xmax / segw) + 1u, b1 / segw), v);
 #if defined(S3R_GEO_ABLATE)                  // timing-only variants: 1 = no segment starts
     if (S3R_GEO_ABLATE & 1) return;
@@ -1031,7 +1059,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order,
                                                   uint32_t host_fill, unsigned long long *chunk_flags,
-                                                  uint32_t fill_tag) {
+                                                  uint32_t fill_tag, uint32_t row_starts) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1127,7 +1155,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
             const uint32_t b = rank / kTPB, lb = 3u * (rank - b * kTPB);
             if (b < kStateBatches) {
                 uint32_t k;
-                (void)start_index(h0.y, xs, &k);
+                (void)start_index(h0.y, xs, &k, row_starts != 0u);
                 const uint4 s0 = me[4], s1 = me[5], s2 = me[6];
                 const float stv[kWaves * 3] = {u2f(s0.x), u2f(s0.y), u2f(s0.z), u2f(s0.w), u2f(s1.x), u2f(s1.y),
                                                u2f(s1.z), u2f(s1.w), u2f(s2.x), u2f(s2.y), u2f(s2.z), u2f(s2.w)};
@@ -1312,7 +1340,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                             v.c = v.k0 == kp ? cp : (v.k0 == kp + 1u ? cp + v.d : walk(cp, v.d, v.k0 - kp S3R_IT(p_chunk)));
                         } else {
                             uint32_t k;
-                            const uint32_t j = start_index(e.xmin, xs, &k);
+                            const uint32_t j = start_index(e.xmin, xs, &k, row_starts != 0u);
                             const float c0v = rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
                             v.c = walk(c0v, v.d, v.k0 - k S3R_IT(p_chunk));
                         }
@@ -2245,7 +2273,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order, const GeoSkyFlags *gsf) {
+                     uint32_t *order, const GeoSkyFlags *gsf, bool row_starts) {
     const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
     if (ntri == 0 || rows_local == 0 || (gsf && nrb > kGeoCntMax)) {
         // nothing to set up (every bin is sky), or more row blocks than counters: k_sky_flags publishes
@@ -2255,7 +2283,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                                   st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
                                   nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
                                   (uint32_t)fragment_bins(W, rows_local), order, nrb,
-                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u});
+                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u);
         }
         if (gsf)
             launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
@@ -2269,17 +2297,18 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? 1u : 0u)),
+    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky);
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u);
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
-                     bool frame_rows, uint32_t host_fill, unsigned long long *chunk_flags, uint32_t fill_tag) {
+                     bool frame_rows, uint32_t host_fill, unsigned long long *chunk_flags, uint32_t fill_tag,
+                     bool row_starts) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2297,11 +2326,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag);
+                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           host_fill, chunk_flags, fill_tag);
+                           host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u);
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in

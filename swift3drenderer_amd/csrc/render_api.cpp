@@ -908,6 +908,10 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     const uint32_t tag = d.frame_no;              // >= 1: frame k's completion tag (wait_set_free)
     // host fill: the geometry launch also publishes the bins' sky flags, as soon as every workgroup's
     // pair reservations are in (one extra workgroup waits for them on per-row-block counters)
+    // delivered frames: the geometry tabulates row starts only, the fragment workgroups walk along
+    // their rows themselves (kernels.hip k_geometry); S3R_ROW_STARTS=0: the full start table
+    static const bool row_starts_env = !getenv("S3R_ROW_STARTS") || atoi(getenv("S3R_ROW_STARTS")) != 0;
+    const bool row_starts = hf != nullptr && row_starts_env;
     GeoSkyFlags gsf{};
     if (hf && hf->flags_dev) {
         if (!d.geo_cnt) {
@@ -920,7 +924,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     }
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
-                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr);
+                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts);
     d.hp.lap(3);
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
@@ -935,7 +939,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
                     lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev ? 1u + hf->gpu_eighths : 0u,
-                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u);
+                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u, row_starts);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));

@@ -22,7 +22,7 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
                      bool frame_rows = false, uint32_t host_fill = 0, unsigned long long *chunk_flags = nullptr,
-                     uint32_t fill_tag = 0);
+                     uint32_t fill_tag = 0, bool row_starts = false);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
 // pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0
@@ -40,6 +40,8 @@ uint64_t fragment_bins(uint32_t W, uint32_t rows_local);
 // headers and pairs, and rowtab (2T x rows_local x start_entries(W) x float4): exact barycentrics of
 // every live slot's bbox rows at x = xmin and at each 384-pixel boundary inside the bbox.
 uint32_t start_entries(uint32_t W);
+// row_starts: rowtab and the pairs get the row starts (x = xmin) only, not the start-table boundaries;
+// the fragment launch reading them must be given row_starts too (its walks then start at xmin).
 // Host fill (render_api.cpp): with gsf the launch also publishes the bins' sky flags as soon as every
 // workgroup's pair reservations are in (see launch_sky_flags for flags / tag / probe / gpu_eighths);
 // geo_cnt: kGeoCounterWords zeroed device words (the launch leaves them 0), one set per launch in flight.
@@ -52,7 +54,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order, const GeoSkyFlags *gsf = nullptr);
+                     uint32_t *order, const GeoSkyFlags *gsf = nullptr, bool row_starts = false);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();
