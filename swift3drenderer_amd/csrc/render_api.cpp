@@ -322,7 +322,8 @@ struct Lib {
     // adaptive host fill: eighths of the sky bins the GPUs write themselves, and the smoothed
     // (fill threads' finish - devices' finish) in microseconds that steers it
     int fill_gpu = -1;
-    double fill_skew_us = 0;
+    double fill_skew_us = 0;                   // smoothed (threads' sky-fill end - devices' end)
+    double fill_eighth_us = 0;                 // smoothed F: the threads' fill time per eighth (0: none yet)
     // s3r_fill_profile: frames, sums of the devices' / fill threads' finish times (ns after the
     // frame's start), and per fill thread its last CPU, summed finish time and pixels
     uint64_t prof_frames = 0, prof_dev_ns = 0, prof_fill_ns = 0, prof_pre_ns = 0, prof_issued_ns = 0, prof_done_ns = 0;
@@ -1120,18 +1121,24 @@ void deliver_part(void *arg, int i) {
 //           ~50 GB/s for the copy, tools/micro/pcie_write.hip).
 //   fill    (host fill) as direct, but typically half the frame's bins are sky -- bins no triangle
 //           meets, all background (render.cpp:282): each device publishes every bin's sky flag as
-//           soon as its geometry is done (k_sky_flags), writes only its covered bins, and the
+//           soon as its geometry has binned the triangles (k_geometry), writes only its covered bins, and the
 //           library's fill threads write the sky bins' background with streaming stores meanwhile.
 //           The link carries the covered bins only; the host's memory writes overlap the GPU's.
 // The host fill is adaptive: with N devices the links carry N times the bytes of one while the fill
-// threads' memory bandwidth stays what it is, so k_sky_flags leaves g/8 of the sky bins (bin % 8 < g)
-// to the GPUs, and after every frame g moves one step towards balance -- up when the fill threads
-// finished later than the devices (smoothed, beyond a dead band), down when the devices did.  Any g
-// gives the same pixels; g = 8 is direct delivery plus the flags.  S3R_FILL_GPU=g fixes it.
+// threads' memory bandwidth stays what it is, so the flags leave g/8 of the sky bins (bin % 8 < g)
+// to the GPUs, and after every frame g moves one step where that shortens the frame.  Moving an
+// eighth to the GPUs adds its bytes to the links (L us) and takes its fill (F us) off the threads:
+// worth it when the threads' sky fill ends more than L after the devices; moving one back is worth
+// it when the devices end more than F after the sky fill (smoothed over frames).  The threads' end
+// itself is no measure: the covered bins' background chunks are filled as the last fragment
+// workgroups finish, so the threads never end much before the devices -- judged by it, g only ever
+// climbed.  Any g gives the same pixels; g = 8 is direct delivery plus the flags.  S3R_FILL_GPU=g
+// fixes it.
 // Auto = host fill.  Tile-path frames and buffers that cannot be page-locked are copied.
 constexpr int kDefaultFillThreads = 4;     // one device; measured: 2 CPU-bound, 8-16 add scheduling jitter (p90)
 constexpr int kDefaultFillThreadsMulti = 8;
-constexpr double kFillDeadbandUs = 15.0;
+constexpr double kLinkBytesPerUs = 52000.0;  // one device's link for delivered pixels (~52 GB/s)
+constexpr double kFillEighthUs0 = 30.0;       // F before the first measurement (4K, 4 threads)
 enum Delivery_ { kAuto = 0, kCopy = 1, kDirect = 2, kFill = 3 };
 
 int delivery_mode() {
@@ -1324,6 +1331,10 @@ struct FillJob {
     std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
     std::chrono::steady_clock::time_point t0;
     std::atomic<int64_t> dev_end_ns{0}, fill_end_ns{0};   // latest finish of a device part / a fill thread
+    // the adaptive split's measures: the first flag any thread saw, the last sky bin a thread filled,
+    // and the sky bins of the frame (the host's and the GPUs')
+    std::atomic<int64_t> flags_ns{INT64_MAX}, sky_end_ns{0};
+    std::atomic<uint64_t> sky_bins{0};
     int64_t issued_ns = 0;                                 // part 0's launches issued
     int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
     uint64_t thread_px[65] = {};
@@ -1381,8 +1392,12 @@ void fill_worker(void *arg, int idx) {
             for (uint64_t k = b; k < b + kFillBlock && k < job.parts[p].bins; k++) pend.push_back((uint64_t)p << 48 | k);
     size_t n = pend.size();
     const auto t0 = std::chrono::steady_clock::now();
+    auto since_start = [&job]() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
+    };
     uint32_t idle = 0;
-    uint64_t px = 0;
+    uint64_t px = 0, sky_bins = 0;
+    int64_t first_flag = -1, sky_end = 0;
     while (n) {
         size_t keep = 0;
         for (size_t i = 0; i < n; i++) {
@@ -1395,6 +1410,8 @@ void fill_worker(void *arg, int idx) {
             if (!(e & kWaitChunks)) {
                 const uint32_t f = __atomic_load_n(fp.flags + b, __ATOMIC_ACQUIRE);
                 if ((f & ~(kSkyBit | kGpuBit)) != fp.tag) { pend[keep++] = e; continue; }
+                if (first_flag < 0) first_flag = since_start();
+                sky_bins += (f & (kSkyBit | kGpuBit)) ? 1u : 0u;
                 if (f & kGpuBit) continue;                      // a sky bin the GPU writes itself
                 if (!(f & kSkyBit)) { pend[keep++] = e | kWaitChunks; continue; }
                 sky = true;
@@ -1409,6 +1426,7 @@ void fill_worker(void *arg, int idx) {
             if (part == 0 && b == 0 && (sky || (mask & 1u)) && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
             px += fill_bin(job, fp, b, sky, mask);
+            if (sky) sky_end = since_start();
         }
         if (keep == n) {
             __builtin_ia32_pause();
@@ -1421,6 +1439,15 @@ void fill_worker(void *arg, int idx) {
     }
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
+    job.sky_bins.fetch_add(sky_bins, std::memory_order_relaxed);
+    if (first_flag >= 0) {
+        int64_t cur = job.flags_ns.load(std::memory_order_relaxed);
+        while (first_flag < cur && !job.flags_ns.compare_exchange_weak(cur, first_flag, std::memory_order_relaxed)) {}
+    }
+    if (sky_end) {
+        int64_t cur = job.sky_end_ns.load(std::memory_order_relaxed);
+        while (sky_end > cur && !job.sky_end_ns.compare_exchange_weak(cur, sky_end, std::memory_order_relaxed)) {}
+    }
     job.thread_px[idx] = px;
     job.thread_cpu[idx] = sched_getcpu();
     job.thread_end_ns[idx] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
@@ -1472,6 +1499,23 @@ void deliver_part_direct(void *arg, int i) {
 // device has no mapping of the buffer (nothing was rendered) -- either way the caller redoes the
 // frame by copy.
 enum MappedResult { kMapped, kStaleMap, kUnmapped };
+
+// One step of the adaptive split (see "deliveries" above) after a host-fill frame.
+void fill_adapt(const FillJob &job, uint32_t nparts) {
+    const double dev = (double)job.dev_end_ns.load() / 1e3, t_flags = (double)job.flags_ns.load() / 1e3;
+    const double sky_end = job.sky_end_ns.load() ? (double)job.sky_end_ns.load() / 1e3 : t_flags;
+    const int host = 8 - g.fill_gpu;
+    if (host > 0 && job.sky_end_ns.load()) {
+        const double f = (sky_end - t_flags) / host;
+        g.fill_eighth_us = g.fill_eighth_us > 0 ? 0.75 * g.fill_eighth_us + 0.25 * f : f;
+    }
+    const double F = g.fill_eighth_us > 0 ? g.fill_eighth_us : kFillEighthUs0;
+    const FillPart &fp = job.parts[0];
+    const double L = (double)job.sky_bins.load() * fp.seg_px * fp.rpb * 4.0 / 8.0 / (kLinkBytesPerUs * nparts);
+    g.fill_skew_us = 0.75 * g.fill_skew_us + 0.25 * (sky_end - dev);
+    if (g.fill_skew_us > L && g.fill_gpu < 8) { g.fill_gpu++; g.fill_skew_us = 0; }
+    else if (-g.fill_skew_us > F && g.fill_gpu > 0) { g.fill_gpu--; g.fill_skew_us = 0; }
+}
 
 MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, bool fill) {
     const Lib::Reg *reg = find_reg(buffer, (size_t)W * H * 4);
@@ -1565,13 +1609,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             g.prof_thread[t].px += job.thread_px[t];
         }
     }
-    if (fill && !getenv("S3R_FILL_GPU")) {
-        // one step towards balance between the fill threads and the devices
-        const double skew = (double)(job.fill_end_ns.load() - job.dev_end_ns.load()) / 1e3;
-        g.fill_skew_us = 0.75 * g.fill_skew_us + 0.25 * skew;
-        if (g.fill_skew_us > kFillDeadbandUs && g.fill_gpu < 8) { g.fill_gpu++; g.fill_skew_us = 0; }
-        else if (g.fill_skew_us < -kFillDeadbandUs && g.fill_gpu > 0) { g.fill_gpu--; g.fill_skew_us = 0; }
-    }
+    if (fill && !getenv("S3R_FILL_GPU") && job.flags_ns.load() != INT64_MAX) fill_adapt(job, nparts);
     // pixel 0 written by the GPU (direct, or a covered chunk under host fill) is a pixel, neither
     // probe, unless the mapping is stale; a pixel 0 the host filled was checked by its fill thread
     bool host0 = false;
