@@ -45,8 +45,11 @@ def main():
         print(k)
         for c in sorted(cs):
             print(f'   {c:28s} {cs[c]:.6g}')
-    # the fragment stage: k_fragment (row path) or k_tile_raster + k_tile_resolve (tile path)
-    stage = [k for k in out if 'k_fragment' in k] or [k for k in out if 'k_tile_raster' in k or 'k_tile_resolve' in k]
+    # the fragment stage: k_fragment (row path; its HBM instance, HOSTW = false -- the delivered
+    # instance's stores go to the host) or k_tile_raster + k_tile_resolve (tile path)
+    frag = [k for k in out if 'k_fragment' in k]
+    stage = ([k for k in frag if k.replace(' ', '').endswith(',false>')] or frag or
+             [k for k in out if 'k_tile_raster' in k or 'k_tile_resolve' in k])
     if stage and a.workload and all('FETCH_SIZE' in out[k] and 'WRITE_SIZE' in out[k] for k in stage):
         fetch = sum(out[k]['FETCH_SIZE'] for k in stage)
         write = sum(out[k]['WRITE_SIZE'] for k in stage)

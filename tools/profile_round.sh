@@ -11,7 +11,7 @@ STEPS=${STEPS:-20}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOTDIR=$(pwd)
-BARGS="--steps $STEPS --warmup 2 --no-cpu-baseline --no-e2e $BENCH_EXTRA"
+BARGS="--steps $STEPS --warmup 2 --no-cpu-baseline $BENCH_EXTRA"
 WORKLOAD=${WORKLOAD:-full/P_over/3840x2160/N1}
 TRACE_ONLY=${TRACE_ONLY:-0}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOTDIR/$OUT/trace" -o run --output-format csv -- python3 bench.py $BARGS > "$OUT/trace.log" 2>&1 || exit 1
