@@ -162,6 +162,12 @@ void s3r_timing_collect(double out[3]);
  * host-buffer registrations updateAndRender found stale and replaced}. */
 void s3r_scene_counts(uint64_t out[8]);
 
+/* Tile path (device 0): out[0] frames whose tile-list size was read back before the fill (one host
+ * sync: asynchronous frames and each buffer set's first), out[1] synchronous updateAndRender frames
+ * whose list, sized by earlier frames, overflowed and that were rendered again, out[2] the last
+ * frame's (tile, triangle) pairs, out[3] 0. */
+void s3r_tile_stats(uint64_t out[4]);
+
 /* Copy the current camera matrix (3 rows x 4) and raster factor. */
 void s3r_camera(float out_matrix[12], float *out_factor);
 

@@ -1583,7 +1583,7 @@ static_assert(kDepthBuckets <= 64, "bucket field of a packed tile box");
 // Per step the groups are found first (ballots only), then every group leader issues its atomic in
 // ONE vector instruction, so a step waits for one atomic round trip, not one per distinct tile.
 __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x, uint32_t *__restrict__ ctr,
-                                           uint32_t *__restrict__ list, uint32_t slot) {
+                                           uint32_t *__restrict__ list, uint32_t slot, uint32_t cap = 0xFFFFFFFFu) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t rounds = sp.n;
     for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
@@ -1618,7 +1618,7 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
 #pragma unroll
             for (uint32_t q = 0; q < kSteps; q++) {
                 const uint32_t b = (uint32_t)__shfl((int)base[q], (int)leader_of[q]);
-                if (k0 + q < sp.n) list[b + rank[q]] = slot;
+                if (k0 + q < sp.n && b + rank[q] < cap) list[b + rank[q]] = slot;   // (past cap: overflow)
             }
         }
     }
@@ -1765,23 +1765,31 @@ __global__ void __launch_bounds__(256) k_tile_cursor(const uint32_t *__restrict_
     if (i == n - 1u) *total = offs[i] + counts[i];
 }
 
-// Scatter: threads [0, ntri) the original triangles (packed bboxes), then the clip-appended slots.
+// Scatter: thread i the original triangle i (packed bbox), then the i-th clip-appended slot if
+// there is one (i < *napp: at most one appended slot per triangle, so the grid covers them).  The
+// list holds cap entries: a frame whose list needs more (sized from an earlier frame, no read-back)
+// writes only those, and the host renders it again with a larger list (render_api.cpp render_tiles).
 __global__ void __launch_bounds__(256) k_tile_fill(const uint32_t *__restrict__ boxes, uint32_t ntri,
                                                    const RasterRec *__restrict__ recs,
-                                                   const uint32_t *__restrict__ app_list, uint32_t napp,
+                                                   const uint32_t *__restrict__ app_list, const uint32_t *__restrict__ napp,
                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
-                                                   uint32_t *__restrict__ cursor, uint32_t *__restrict__ list) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t bx = kDeadBox, by = 0, slot = 0;
+                                                   uint32_t *__restrict__ cursor, uint32_t *__restrict__ list, uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, na = *napp;
+    uint32_t bx = kDeadBox, by = 0;
     if (i < ntri) {
         const uint2 b = reinterpret_cast<const uint2 *>(boxes)[i];
-        bx = b.x; by = b.y; slot = i;
-    } else if (i - ntri < napp) {
-        slot = app_list[i - ntri];
+        bx = b.x; by = b.y;
+    }
+    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, i, cap);
+    if (__ballot(i < na) == 0) return;                    // (wave-uniform: no appended slot for this wave)
+    uint32_t slot = 0;
+    bx = kDeadBox; by = 0;
+    if (i < na) {
+        slot = app_list[i];
         const uint4 h = reinterpret_cast<const uint4 *>(recs + slot)[0];
         bx = tile_box(h.x, h.w); by = h.y;
     }
-    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, slot);
+    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, slot, cap);
 }
 
 struct TileShared {
@@ -1830,7 +1838,8 @@ __device__ __forceinline__ void slot_setup(uint32_t s, uint32_t ntri, const floa
 __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ counts,
-    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys) {
+    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, const uint32_t *__restrict__ total,
+    uint32_t cap) {
     __shared__ TileShared ls;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
@@ -1840,7 +1849,8 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
     // the tile's list: its depth buckets, nearest first, one after another
     const uint32_t s0 = tile * kDepthBuckets, sl = s0 + kDepthBuckets - 1u;
-    const uint32_t base = offs[s0], n = offs[sl] + counts[sl] - base;
+    // a list longer than its buffer (overflow, see k_tile_fill) is incomplete: the frame is redone
+    const uint32_t base = offs[s0], n = *total > cap ? 0u : offs[sl] + counts[sl] - base;
     if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
     // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
     // while stage c0's items run
@@ -2403,22 +2413,31 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        cursor, total);
 }
 
-void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
-                      uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
-                      hipStream_t st) {
-    const uint64_t n = (uint64_t)ntri + napp;
-    if (n == 0) return;
-    hipLaunchKernelGGL(k_tile_fill, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, boxes, ntri,
-                       (const RasterRec *)recs, app_list, napp, band, nparts, part, tile_grid_x(W), cursor, list);
+void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
+                        uint32_t *total, hipStream_t st) {
+    const uint64_t ns = tile_slots(W, rows_local);
+    if (ns == 0) return;
+    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
+                       cursor, total);
+}
+
+void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list,
+                      const uint32_t *napp, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor,
+                      uint32_t *list, uint64_t cap, hipStream_t st) {
+    if (ntri == 0) return;
+    hipLaunchKernelGGL(k_tile_fill, dim3((ntri + 255) / 256), dim3(256), 0, st, boxes, ntri, (const RasterRec *)recs,
+                       app_list, napp, band, nparts, part, tile_grid_x(W), cursor, list,
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
 }
 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, hipStream_t st) {
+                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st) {
     const uint32_t nt = tile_count(W, rows_local);
     if (nt == 0) return;
     hipLaunchKernelGGL(k_tile_raster, dim3(nt), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band, nparts,
-                       part, rows_local, tile_grid_x(W), offs, counts, list, keys);
+                       part, rows_local, tile_grid_x(W), offs, counts, list, keys, total,
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
 }
 
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,

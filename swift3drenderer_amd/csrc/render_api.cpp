@@ -124,7 +124,13 @@ struct Dev {
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
-    uint32_t *tile_total_host = nullptr;       // pinned: (total, appended) per buffer set
+    uint32_t *tile_total_host = nullptr;       // pinned: (appended, total) per buffer set
+    // a synchronous tile-path frame awaiting its overflow check (tile_redo_if_overflowed): its set
+    // and what its fragment stage needs to run again
+    bool tile_pending = false;
+    uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
+    uint32_t *tile_out = nullptr;
+    uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
@@ -734,8 +740,59 @@ bool use_tile_path() {
     return 2ull * g.ntri > kRowPathMaxSlots;
 }
 
+// The tile path's fill and fragment stage of buffer set p (its setup done): scatter into the set's
+// list (capacity d.tile_list_cap[p]), raster, resolve into out, on st after the geometry stream.
+void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                         uint32_t rows_local, uint32_t *out, hipStream_t geo, hipStream_t st, TimingSlot *ts) {
+    const float sw = (float)W, sh = (float)d.tile_H;
+    launch_tile_fill(d.boxes[p], g.ntri, d.recs[p], d.app_list[p], d.app_count[p], W, band, nparts, part,
+                     d.tile_cursor[p], d.tile_list[p], d.tile_list_cap[p], geo);
+    HIPCHECK(hipEventRecord(d.geo_done[p], geo));
+    follow_previous_frame(d, st);
+    HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
+    if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
+    launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p], d.tile_list[p],
+                       d.keys, d.tile_total[p], d.tile_list_cap[p], st);
+    launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
+    if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
+    HIPCHECK(hipEventRecord(d.frag_done[p], st));
+    HIPCHECK(hipGetLastError());
+}
+
+void grow_tile_list(Dev &d, uint32_t p, uint64_t total) {
+    if (d.tile_list_cap[p] >= total && d.tile_list_cap[p] > 0) return;
+    HIPCHECK(hipDeviceSynchronize());
+    if (d.tile_list[p]) HIPCHECK(hipFree(d.tile_list[p]));
+    // a quarter of headroom (S3R_TILE_LIST_EXACT=1, tests: none, so the next larger frame overflows)
+    const bool exact = getenv("S3R_TILE_LIST_EXACT") && atoi(getenv("S3R_TILE_LIST_EXACT")) != 0;
+    const uint64_t cap = exact ? (total ? total : 1) : total + total / 4 + 1024;
+    d.tile_list[p] = dalloc<uint32_t>(cap);
+    d.tile_list_cap[p] = cap;
+}
+
+// After a synchronous tile-path frame (its stream drained): if its list overflowed the capacity the
+// set had from earlier frames, render its fragment stage again into a list of the right size and
+// return true (the caller redoes its delivery); the totals are in tile_total_host by then.
+bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
+    if (!d.tile_pending) return false;
+    d.tile_pending = false;
+    const uint32_t p = d.tile_pending_set;
+    const uint64_t total = d.tile_total_host[2 * p + 1];
+    d.last_pairs = total;
+    if (total <= d.tile_list_cap[p]) return false;
+    d.tile_overflows++;
+    grow_tile_list(d, p, total);
+    hipStream_t geo = d.geo[0];
+    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_total[p], geo);
+    tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
+                        nullptr);
+    HIPCHECK(hipStreamSynchronize(st));
+    return true;
+}
+
 void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                  uint32_t *out, hipStream_t st, TimingSlot *ts) {
+                  uint32_t *out, hipStream_t st, TimingSlot *ts, bool sync) {
     if (W > 65535 || H > 65535) {                       // packed 16-bit bboxes
         fprintf(stderr, "s3r: tile path supports frames up to 65535 x 65535\n");
         exit(1);
@@ -792,34 +849,31 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.boxes[p], d.app_list[p], d.app_count[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
                       d.tile_total[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv);
-    // the list size is data-dependent: read it back (the tile path's one host sync per frame)
+    // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
+    // of each buffer set, read it back before the fill (one host sync); synchronous frames
+    // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are
+    // rendered again after the frame if it overflowed (tile_redo_if_overflowed; the fill and raster
+    // kernels bound their list accesses).  S3R_TILE_READBACK=1: always read back.
+    const bool readback_env = getenv("S3R_TILE_READBACK") && atoi(getenv("S3R_TILE_READBACK")) != 0;
     uint32_t *host = d.tile_total_host + 2 * p;
-    HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
-    HIPCHECK(hipStreamSynchronize(geo));
-    const uint32_t napp = host[0];
-    const uint64_t total = host[1];
-    d.last_pairs = total;
     d.last_path = 2;
-    if (d.tile_list_cap[p] < total) {
-        HIPCHECK(hipDeviceSynchronize());
-        if (d.tile_list[p]) HIPCHECK(hipFree(d.tile_list[p]));
-        const uint64_t cap = total + total / 4 + 1024;
-        d.tile_list[p] = dalloc<uint32_t>(cap);
-        d.tile_list_cap[p] = cap;
+    d.tile_H = H;
+    if (!sync || d.tile_list_cap[p] == 0 || readback_env) {
+        HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
+        HIPCHECK(hipStreamSynchronize(geo));
+        d.last_pairs = host[1];
+        d.tile_readbacks++;
+        grow_tile_list(d, p, host[1]);
     }
-    launch_tile_fill(d.boxes[p], g.ntri, d.recs[p], d.app_list[p], napp, W, band, nparts, part, d.tile_cursor[p],
-                     d.tile_list[p], geo);
-    HIPCHECK(hipEventRecord(d.geo_done[p], geo));
-    follow_previous_frame(d, st);
-    HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
-    if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p], d.tile_list[p],
-                       d.keys, st);
-    launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
-    if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
-    HIPCHECK(hipEventRecord(d.frag_done[p], st));
-    HIPCHECK(hipGetLastError());
+    tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts);
+    if (sync) {
+        // this frame's totals to the host, for the overflow check once the frame is done
+        HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        d.tile_pending = true;
+        d.tile_pending_set = p;
+        d.tile_W = W; d.tile_band = band; d.tile_nparts = nparts; d.tile_part = part; d.tile_rows = rows_local;
+        d.tile_out = out;
+    }
 }
 
 // A frame part written straight into the caller's mapped host buffer (direct / host-fill delivery):
@@ -847,7 +901,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
                  uint32_t *out, hipStream_t st, const HostFill *hf = nullptr, bool sync = false) {
     TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
-        render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts);
+        render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts, sync);
         return;
     }
     d.last_path = 1;
@@ -1108,6 +1162,16 @@ void deliver_part(void *arg, int i) {
         }
     }
     HIPCHECK(hipStreamSynchronize(d.stream));
+    if (rows && job.W && tile_redo_if_overflowed(d, d.stream)) {
+        // the tile list was too short for this frame: rendered again, delivered again
+        if (job.nparts == 1) {
+            if (job.copy_bytes)
+                HIPCHECK(hipMemcpyAsync(job.host, d.frame, job.copy_bytes, hipMemcpyDeviceToHost, d.stream));
+        } else {
+            copy_bands_to_host(d.frame, job.W, job.H, job.band, job.nparts, (uint32_t)i, job.host, d.stream);
+        }
+        HIPCHECK(hipStreamSynchronize(d.stream));
+    }
 }
 
 // ---------------------------------------------------------------- deliveries
@@ -1880,6 +1944,14 @@ __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
     out[5] = d ? d->last_pairs : 0;          // tile path: (slot, tile) pairs binned last frame
     out[6] = d ? (uint64_t)d->last_path : 0; // fragment stage of the last frame: 1 rows, 2 tiles
     out[7] = g.stale_pins;                   // stale host registrations replaced by updateAndRender
+}
+
+__attribute__((visibility("default"))) void s3r_tile_stats(uint64_t out[4]) {
+    const Dev *d = g.devs.empty() ? nullptr : g.devs[0];
+    out[0] = d ? d->tile_readbacks : 0;      // frames whose list size was read back before the fill
+    out[1] = d ? d->tile_overflows : 0;      // synchronous frames rendered again into a larger list
+    out[2] = d ? d->last_pairs : 0;
+    out[3] = 0;
 }
 
 __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {

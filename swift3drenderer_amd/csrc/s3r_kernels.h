@@ -95,13 +95,20 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        hipStream_t st, float4 *vrv = nullptr, uint32_t nv = 0);
 // vrv (nv float4, may be null): run the vertex stage first (k_tile_vertex) and set triangles up
 // from its projected vertices.
-void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list, uint32_t napp,
-                      uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list,
-                      hipStream_t st);
+// napp: device word, the appended slots' count (app_list's length); list: cap entries -- a frame whose
+// list (*total entries, device word) needs more writes only cap of them, and k_tile_raster then
+// renders no triangle (the caller renders the frame again with a larger list).
+// The fill's scatter cursors reset to the offsets (as launch_tile_setup leaves them): a frame's fill
+// again, e.g. into a larger list after an overflow.
+void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
+                        uint32_t *total, hipStream_t st);
+void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list,
+                      const uint32_t *napp, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor,
+                      uint32_t *list, uint64_t cap, hipStream_t st);
 // keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, hipStream_t st);
+                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st);
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,

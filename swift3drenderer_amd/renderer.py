@@ -20,7 +20,7 @@ EXPORTS = ['updateAndRender', 's3r_configure', 's3r_configure_devices', 's3r_dev
            's3r_set_raster_path', 's3r_raster_path', 's3r_unregister_host', 's3r_host_pinned', 's3r_host_stats',
            's3r_render_bands', 's3r_bands_to_host', 's3r_band_rows_local', 's3r_timing', 's3r_timing_collect',
            's3r_scene_counts', 's3r_camera', 's3r_debug_set_frame_count', 's3r_set_delivery', 's3r_delivery',
-           's3r_fill_profile']
+           's3r_fill_profile', 's3r_tile_stats']
 
 _lib = None
 # host frames of update_and_render(out=None), one per shape, kept for the process: the library may
@@ -75,6 +75,8 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_delivery.restype = ctypes.c_int
     lib.s3r_fill_profile.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
     lib.s3r_fill_profile.restype = ctypes.c_uint32
+    lib.s3r_tile_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    lib.s3r_tile_stats.restype = None
     missing = [name for name in EXPORTS if not hasattr(lib, name)]
     if missing:
         raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
@@ -138,6 +140,12 @@ class Renderer:
                 'node': ctypes.c_int64(out[7]).value,
                 'threads': [{'cpu': int(out[8 + 4 * t]), 'end_us': us(out[9 + 4 * t]), 'px': int(out[10 + 4 * t] // f)}
                             for t in range(n)]}
+
+    def tile_stats(self) -> dict:
+        """Tile path list sizing (include/render.h s3r_tile_stats)."""
+        out = (ctypes.c_uint64 * 4)()
+        self.lib.s3r_tile_stats(out)
+        return {'readbacks': int(out[0]), 'overflows': int(out[1]), 'last_pairs': int(out[2])}
 
     DELIVERIES = {'env': -1, 'auto': 0, 'copy': 1, 'direct': 2, 'fill': 3}
 

@@ -167,3 +167,29 @@ def test_vertex_stage_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeyp
         assert np.array_equal(got, want), diff(got, want)
     finally:
         gpu_renderer.set_raster_path('auto')
+
+
+def test_sync_frames_without_list_readback(gpu_renderer, icosa_dir, monkeypatch):
+    """updateAndRender frames on the tile path size each buffer set's list from earlier frames (no
+    host sync before the fill); a frame whose list overflowed is rendered again into a larger one.
+    With no headroom (S3R_TILE_LIST_EXACT=1) walking towards the icosahedra grows the list every
+    few frames: every frame must still equal the oracle's, and some must have been redone."""
+    from oracle.oracle import OracleRenderer
+    monkeypatch.setenv('S3R_TILE_LIST_EXACT', '1')
+    path = icosa_dir[2000]
+    r = gpu_renderer
+    r.configure(path)
+    r.set_raster_path('tiles')
+    try:
+        o = OracleRenderer(path)
+        w, h = 640, 480
+        seq = [(0, 0, 0, 0, 0, 0)] + [(40.0, 0, 0, 0, 0.0, 0.0)] * 14 + [(0, 0, 0, 0, 25.0, -10.0)] * 3
+        out = np.empty((h, w), dtype=np.uint32)
+        for k, inp in enumerate(seq):
+            got = r.update_and_render(w, h, inp, out)
+            want = o.update_and_render(w, h, inp)
+            assert np.array_equal(got, want), f'frame {k}: ' + diff(got, want)
+        st = r.tile_stats()
+        assert st['overflows'] > 0 and st['readbacks'] <= 4 + st['overflows'], st
+    finally:
+        r.set_raster_path('auto')
