@@ -934,7 +934,9 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     // the chip): a frame part of one round gains nothing and would pay the order column's time
     const uint64_t bins = nbins;
     const char *lpt_env = getenv("S3R_LPT_MIN");            // tuning / test override
-    const bool lpt = g.ntri > 0 && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins);
+    // (delivered frames are bound by the link, not by their heaviest bins: launch order, no order
+    // column; measured equal or 1 us better)
+    const bool lpt = g.ntri > 0 && !hf && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins);
     if (lpt && d.order_cap < bins) {
         HIPCHECK(hipDeviceSynchronize());
         for (int q = 0; q < kSets; q++) {
