@@ -143,8 +143,9 @@ int s3r_set_delivery(int mode, int fill_threads);
  * out[5] fill threads joined; out[6] 1 if the fill threads are placed one per CPU domain, out[7]
  * the NUMA node of the buffer they were placed for (int64, -1 unknown); for fill thread t = 1..n at
  * out[8 + 4(t - 1)]: the CPU it last ran on,
- * its summed finish time, the pixels it wrote.  Returns n (<= max_threads); out holds
- * 8 + 4 * max_threads words. */
+ * its summed finish time, the background pixels it wrote, its summed time in covered bins (their
+ * background chunks, and the widening of staged chunks under the packed delivery).  Returns n
+ * (<= max_threads); out holds 8 + 4 * max_threads words. */
 uint32_t s3r_fill_profile(uint64_t *out, uint32_t max_threads);
 int s3r_delivery(void);
 

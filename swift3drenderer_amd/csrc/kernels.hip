@@ -1059,7 +1059,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order,
                                                   uint32_t host_fill, unsigned long long *chunk_flags,
-                                                  uint32_t fill_tag, uint32_t row_starts) {
+                                                  uint32_t fill_tag, uint32_t row_starts,
+                                                  uint8_t *__restrict__ pstage) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1214,6 +1215,24 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         const uint32_t o = lane >= rsh ? rot : carry;
         if (o != kNoPixel) row[c0x - rsh + lane] = o;
         carry = rot;
+    };
+    // HOSTW with pstage (packed delivery, render_api.cpp): a whole covered chunk goes over the link
+    // at 3 bytes a pixel into the staging frame (row y at stage + 3 W y) -- 192 bytes, lanes 0..47 one
+    // dword each, gathered from the lanes of its pixels -- and the host widens it into the caller's
+    // buffer once the bin's chunk mask is in; a chunk cut by the frame's right edge is stored
+    // directly.  The link carries 3/4 of the covered pixels' bytes.
+    uint8_t *const srow = (HOSTW && pstage) ? pstage + (size_t)3u * W * y : nullptr;
+    auto put_packed = [&](uint32_t c0x, uint32_t v) {
+        const uint32_t b = 4u * lane, i0 = b / 3u, o = b - 3u * i0;
+        const uint32_t a0 = (uint32_t)__shfl((int)v, (int)min(i0, 63u));
+        const uint32_t a1 = (uint32_t)__shfl((int)v, (int)min(i0 + 1u, 63u));
+        const uint32_t w = o == 0u ? (a0 & 0xFFFFFFu) | (a1 << 24) : o == 1u ? ((a0 >> 8) & 0xFFFFu) | (a1 << 16)
+                                                                          : ((a0 >> 16) & 0xFFu) | (a1 << 8);
+        // system-scope stores: their completion (the s_waitcnt before the chunk mask) is their arrival
+        // in host memory, so the host never reads a staged chunk before its bytes
+        if (lane < 48u)
+            __hip_atomic_store(reinterpret_cast<uint32_t *>(srow + 3u * c0x) + lane, w, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     };
     S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
@@ -1391,12 +1410,20 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 512)     // ablation: every shade reads one record
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #else
+            // (packed: a whole chunk of a valid row; kPX == 1, row_ok is wave-uniform)
+            const bool packed = HOSTW && kPX == 1u && srow != nullptr && row_ok && cx0 + kChunk - 1u <= xe;
             if (!WF) {
                 const bool act = row_ok && xp <= xe;
                 uint32_t px = kNoPixel;
                 if (act) px = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
-                if (HOSTW) put(cx0 + 64u * p, px);
-                else if (act) row[xp] = px;
+                if (packed) {
+                    put_packed(cx0, px);
+                    put(cx0 + 64u * p, kNoPixel);
+                } else if (HOSTW) {
+                    put(cx0 + 64u * p, px);
+                } else if (act) {
+                    row[xp] = px;
+                }
             } else {
                 // waterfall over the wave's distinct winners (usually one: a chunk inside one
                 // triangle): each round shades the lanes of one winner, whose record address is
@@ -1420,8 +1447,14 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                         px = shade_core_flat(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
                                              depth[p], tex, ntex);
                 }
-                if (HOSTW) put(cx0 + 64u * p, act ? px : kNoPixel);
-                else if (act) row[xp] = px;
+                if (packed) {
+                    put_packed(cx0, px);
+                    put(cx0 + 64u * p, kNoPixel);
+                } else if (HOSTW) {
+                    put(cx0 + 64u * p, act ? px : kNoPixel);
+                } else if (act) {
+                    row[xp] = px;
+                }
             }
 #endif
 #endif
@@ -1430,7 +1463,10 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     }
     if (HOSTW && rsh != 0u && lane < rsh && carry != kNoPixel) row[cx_next - rsh + lane] = carry;
     if (HOSTW && host_fill) {
-        // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q)
+        // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q).  With staged
+        // chunks, every wave's stores are complete before the mask is stored after them: the host
+        // reads the staging frame once it sees the mask (both cross the link in that order)
+        if (pstage) __builtin_amdgcn_s_waitcnt(0);
         if (lane == 0) sh.bgm[wave] = bgm;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2318,7 +2354,7 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
                      bool frame_rows, uint32_t host_fill, unsigned long long *chunk_flags, uint32_t fill_tag,
-                     bool row_starts) {
+                     bool row_starts, uint8_t *stage) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2336,11 +2372,11 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     if (done)
         hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u);
+                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u, stage);
     else
         hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u);
+                           host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u, stage);
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in

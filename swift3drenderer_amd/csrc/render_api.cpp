@@ -42,6 +42,7 @@
 
 namespace s3r_host {   // host_fill.cpp
 void fill_words(uint32_t *p, size_t n, uint32_t v);
+void widen_pixels(const uint8_t *src, uint32_t *dst, size_t n);
 void store_fence();
 }
 
@@ -142,6 +143,8 @@ struct Dev {
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
     uint32_t *geo_cnt = nullptr;             // host fill: per buffer set, k_geometry's bin-phase count
+    uint8_t *stage_dev = nullptr;            // packed delivery: this device's address of Lib::stage
+    uint64_t stage_epoch = 0;
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
     // the previous frame's stream; NULL is a valid caller stream (the legacy default stream), so
     // whether a previous frame exists is its own flag
@@ -323,6 +326,10 @@ struct Lib {
     int fill_threads = -1;                     // host fill threads; -1: S3R_FILL_THREADS or the default
     Pool fill_pool;
     int fill_node = -2;                        // NUMA node the fill threads were placed for
+    uint8_t *stage = nullptr;                  // packed delivery: the staging frame (host, 3 B a pixel)
+    size_t stage_cap = 0;
+    uint64_t stage_epoch = 0;                  // bumped when the staging frame is reallocated
+    int pack = -1;                             // packed delivery: -1 unset (S3R_PACK, default on)
     bool fill_placed = false;                  // fill threads pinned one per CPU domain (fill_placement)
     uint64_t copy_frames = 0, direct_frames = 0, fill_frames = 0;
     // adaptive host fill: eighths of the sky bins the GPUs write themselves, and the smoothed
@@ -334,7 +341,7 @@ struct Lib {
     // frame's start), and per fill thread its last CPU, summed finish time and pixels
     uint64_t prof_frames = 0, prof_dev_ns = 0, prof_fill_ns = 0, prof_pre_ns = 0, prof_issued_ns = 0, prof_done_ns = 0;
     std::chrono::steady_clock::time_point call_t0;     // updateAndRender's entry (the profile's pre_ns)
-    struct ThreadProf { int64_t cpu = -1; uint64_t end_ns = 0, px = 0; } prof_thread[65];
+    struct ThreadProf { int64_t cpu = -1; uint64_t end_ns = 0, px = 0, covered_ns = 0; } prof_thread[65];
     bool unmapped = false;                     // a device could not map a caller buffer: copy only
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
@@ -600,6 +607,14 @@ void dev_release(Dev &d) {
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
+void free_stage() {
+    if (!g.stage) return;
+    (void)hipHostUnregister(g.stage);
+    free(g.stage);
+    g.stage = nullptr;
+    g.stage_cap = 0;
+}
+
 void release_all() {
     g.pool.stop();
     g.fill_pool.stop();
@@ -609,6 +624,7 @@ void release_all() {
             (void)hipDeviceSynchronize();
         }
         unregister_all();
+        free_stage();
         for (Dev *d : g.devs) {
             dev_release(*d);
             delete d;
@@ -886,6 +902,7 @@ struct HostFill {
     uint32_t *probe_dev;
     unsigned long long *chunks_dev;
     uint32_t gpu_eighths;     // sky bins with bin % 8 below this stay with the GPU (adaptive split)
+    uint8_t *stage_dev;       // packed delivery: the device's address of the staging frame (or null)
 };
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
@@ -996,7 +1013,8 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
                     lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev ? 1u + hf->gpu_eighths : 0u,
-                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u, row_starts);
+                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u, row_starts,
+                    hf && hf->flags_dev ? hf->stage_dev : nullptr);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -1364,6 +1382,15 @@ std::vector<cpu_set_t> fill_placement(int threads, int node) {
     return out;
 }
 
+// Packed delivery (host fill): whole covered chunks cross the link at 3 bytes a pixel into a
+// staging frame and the fill threads widen them into the caller's buffer (kernels.hip k_fragment,
+// host_fill.cpp widen_pixels) -- the link carries a quarter fewer bytes, the host writes the covered
+// pixels too.  Opt-in while its host side is tuned: S3R_PACK=1.
+bool pack_enabled() {
+    if (g.pack < 0) g.pack = getenv("S3R_PACK") && atoi(getenv("S3R_PACK")) == 1 ? 1 : 0;
+    return g.pack == 1;
+}
+
 // Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override):
 // by default 4 (one device) or 8, but no more than the CPUs left beside the calling thread and the
 // nparts - 1 device workers.
@@ -1394,7 +1421,9 @@ struct FillJob {
     FillPart parts[kMaxDevices];
     HostFill hf[kMaxDevices];
     std::atomic<bool> stale{false};  // pixel 0 checked before its bin was filled: the mapping is stale
-    std::atomic<uint64_t> sky_px{0}; // pixels the fill threads wrote
+    std::atomic<uint64_t> sky_px{0}; // background pixels the fill threads wrote
+    std::atomic<uint64_t> packed_px{0};  // staged pixels they widened (packed delivery)
+    const uint8_t *stage = nullptr;  // packed delivery: the staging frame (host address), else null
     std::chrono::steady_clock::time_point t0;
     std::atomic<int64_t> dev_end_ns{0}, fill_end_ns{0};   // latest finish of a device part / a fill thread
     // the adaptive split's measures: the first flag any thread saw, the last sky bin a thread filled,
@@ -1404,6 +1433,7 @@ struct FillJob {
     int64_t issued_ns = 0;                                 // part 0's launches issued
     int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
     uint64_t thread_px[65] = {};
+    int64_t thread_widen_ns[65] = {};  // time in covered bins (widening, their background chunks)
     int thread_cpu[65] = {};
 };
 
@@ -1415,11 +1445,27 @@ void note_end(const FillJob &job, std::atomic<int64_t> &end) {
 
 // Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
 // row_in_bin * chunks_per_row + chunk) of a covered bin; returns the pixels written.
-uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, uint32_t mask) {
+// Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
+// row_in_bin * chunks_per_row + chunk) of a covered bin -- and, with the packed delivery, widens
+// the covered bin's staged chunks (every other chunk wholly inside the frame) into the frame;
+// returns the background pixels written, *packed += the pixels widened.
+uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, uint32_t mask, uint64_t *packed) {
     const uint32_t blk = (uint32_t)(b / fp.segs), seg = (uint32_t)(b % fp.segs);
     const uint32_t xs = seg * fp.seg_px, xe = xs + fp.seg_px < job.W ? xs + fp.seg_px : job.W;
     const uint32_t cpr = fp.seg_px / fp.chunk_px;
     uint64_t px = 0;
+    if (!sky && job.stage) {
+        // the bin's staged rows are cold (just written by the device): request all their lines at
+        // once, so the widening below waits for memory once per bin, not once per chunk
+        for (uint32_t k = 0; k < fp.rpb; k++) {
+            const uint32_t lr = blk * fp.rpb + k;
+            if (lr >= fp.rows_local) break;
+            const uint32_t y = ((lr / fp.band) * fp.nparts + fp.part) * fp.band + lr % fp.band;
+            if (y >= job.H) continue;
+            const uint8_t *a = job.stage + 3 * ((size_t)y * job.W + xs), *e = job.stage + 3 * ((size_t)y * job.W + xe);
+            for (; a < e; a += 64) __builtin_prefetch(a, 0, 0);
+        }
+    }
     for (uint32_t k = 0; k < fp.rpb; k++) {
         const uint32_t lr = blk * fp.rpb + k;
         if (lr >= fp.rows_local) break;
@@ -1432,11 +1478,15 @@ uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, 
             continue;
         }
         for (uint32_t q = 0; q < cpr; q++) {
-            if (!((mask >> (k * cpr + q)) & 1u)) continue;
             const uint32_t c0 = xs + q * fp.chunk_px, c1 = c0 + fp.chunk_px < xe ? c0 + fp.chunk_px : xe;
             if (c0 >= c1) continue;
-            s3r_host::fill_words(row + c0, c1 - c0, kBackground);
-            px += c1 - c0;
+            if ((mask >> (k * cpr + q)) & 1u) {
+                s3r_host::fill_words(row + c0, c1 - c0, kBackground);
+                px += c1 - c0;
+            } else if (job.stage && c1 - c0 == fp.chunk_px) {
+                s3r_host::widen_pixels(job.stage + 3 * ((size_t)y * job.W + c0), row + c0, fp.chunk_px);
+                *packed += fp.chunk_px;
+            }
         }
     }
     return px;
@@ -1462,7 +1512,8 @@ void fill_worker(void *arg, int idx) {
         return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     };
     uint32_t idle = 0;
-    uint64_t px = 0, sky_bins = 0;
+    uint64_t px = 0, sky_bins = 0, packed = 0;
+    int64_t widen_ns = 0;
     int64_t first_flag = -1, sky_end = 0;
     while (n) {
         size_t keep = 0;
@@ -1485,13 +1536,21 @@ void fill_worker(void *arg, int idx) {
                 const unsigned long long c = __atomic_load_n(fp.chunks + b, __ATOMIC_ACQUIRE);
                 if ((uint32_t)(c >> 32) != fp.tag) { pend[keep++] = e; continue; }
                 mask = (uint32_t)c;
-                if (!mask) continue;
+                if (!mask && !job.stage) continue;
             }
-            // pixel 0 (part 0, bin 0, its first row and chunk): the sky-flag kernel wrote kMapProbe
-            // there through its mapping before publishing the bin's flag
-            if (part == 0 && b == 0 && (sky || (mask & 1u)) && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
+            // pixel 0 (part 0, bin 0, its first row and chunk): the flag publisher wrote kMapProbe
+            // there through its mapping before publishing the bin's flag; the host writes pixel 0 when
+            // the chunk is background or staged (packed delivery)
+            if (part == 0 && b == 0 && (sky || (mask & 1u) || (job.stage && fp.rows_local && job.W >= fp.chunk_px)) &&
+                __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
-            px += fill_bin(job, fp, b, sky, mask);
+            if (!sky && job.stage) {
+                const auto w0 = std::chrono::steady_clock::now();
+                px += fill_bin(job, fp, b, sky, mask, &packed);
+                widen_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+            } else {
+                px += fill_bin(job, fp, b, sky, mask, &packed);
+            }
             if (sky) sky_end = since_start();
         }
         if (keep == n) {
@@ -1505,6 +1564,7 @@ void fill_worker(void *arg, int idx) {
     }
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
+    job.packed_px.fetch_add(packed, std::memory_order_relaxed);
     job.sky_bins.fetch_add(sky_bins, std::memory_order_relaxed);
     if (first_flag >= 0) {
         int64_t cur = job.flags_ns.load(std::memory_order_relaxed);
@@ -1515,6 +1575,7 @@ void fill_worker(void *arg, int idx) {
         while (sky_end > cur && !job.sky_end_ns.compare_exchange_weak(cur, sky_end, std::memory_order_relaxed)) {}
     }
     job.thread_px[idx] = px;
+    job.thread_widen_ns[idx] = widen_ns;
     job.thread_cpu[idx] = sched_getcpu();
     job.thread_end_ns[idx] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     note_end(job, job.fill_end_ns);
@@ -1617,6 +1678,34 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             g.fill_placed = !cpus.empty();
         }
     }
+    // packed delivery (host fill only): the staging frame, 3 bytes a pixel, mapped on every device
+    if (fill && pack_enabled()) {
+        // ordinary (CPU-cacheable) pages, registered plainly for the devices: the fill threads read
+        // it at memory speed (hipHostMalloc's pages, or an uncached registration, read ~10x slower);
+        // its rows are 64-B aligned, so the GPUs' whole-line stores need no uncached mapping
+        const size_t bytes = ((size_t)3 * W * H + 64 + 4095) & ~(size_t)4095;
+        if (g.stage_cap < bytes) {
+            drain_devices();
+            HIPCHECK(hipSetDevice(g.devs[0]->device));
+            free_stage();
+            void *p = aligned_alloc(4096, bytes);
+            if (!p) { fprintf(stderr, "s3r: staging frame allocation failed\n"); exit(1); }
+            memset(p, 0, bytes);
+            HIPCHECK(hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
+            g.stage = static_cast<uint8_t *>(p);
+            g.stage_cap = bytes;
+            g.stage_epoch++;
+        }
+        job.stage = g.stage;
+        for (uint32_t i = 0; i < nparts; i++) {
+            Dev &d = *g.devs[i];
+            if (d.stage_epoch != g.stage_epoch) {
+                HIPCHECK(hipSetDevice(d.device));
+                HIPCHECK(hipHostGetDevicePointer((void **)&d.stage_dev, g.stage, 0));
+                d.stage_epoch = g.stage_epoch;
+            }
+        }
+    }
     const uint32_t band = nparts == 1 ? H : g.band;
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
@@ -1627,7 +1716,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
         fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
         if (!fill) {
-            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0};
+            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0, nullptr};
             continue;
         }
         if (d.fill_cap < fp.bins) {
@@ -1652,7 +1741,8 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
         fp.flags = d.fill_flags;
         fp.chunks = d.fill_chunks;
         fp.tag = d.fill_tag;
-        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu};
+        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu,
+                             job.stage ? d.stage_dev : nullptr};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
@@ -1673,6 +1763,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             g.prof_thread[t].cpu = job.thread_cpu[t];
             g.prof_thread[t].end_ns += (uint64_t)job.thread_end_ns[t];
             g.prof_thread[t].px += job.thread_px[t];
+            g.prof_thread[t].covered_ns += (uint64_t)job.thread_widen_ns[t];
         }
     }
     if (fill && !getenv("S3R_FILL_GPU") && job.flags_ns.load() != INT64_MAX) fill_adapt(job, nparts);
@@ -1681,11 +1772,12 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
     bool host0 = false;
     if (fill && job.parts[0].bins) {
         const uint32_t f0 = job.parts[0].flags[0];
-        host0 = (f0 & kSkyBit) || (!(f0 & kGpuBit) && (job.parts[0].chunks[0] & 1ull));
+        host0 = (f0 & kSkyBit) ||
+                (!(f0 & kGpuBit) && ((job.parts[0].chunks[0] & 1ull) || (job.stage && W >= job.parts[0].chunk_px)));
     }
     const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
     (fill ? g.fill_frames : g.direct_frames)++;
-    g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load());
+    g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load() - job.packed_px.load()) + 3 * job.packed_px.load();
     return stale ? kStaleMap : kMapped;
 }
 
@@ -1896,7 +1988,7 @@ __attribute__((visibility("default"))) uint32_t s3r_fill_profile(uint64_t *out, 
         o[0] = (uint64_t)g.prof_thread[t].cpu;
         o[1] = g.prof_thread[t].end_ns;
         o[2] = g.prof_thread[t].px;
-        o[3] = 0;
+        o[3] = g.prof_thread[t].covered_ns;
     }
     g.prof_frames = g.prof_dev_ns = g.prof_fill_ns = g.prof_pre_ns = g.prof_issued_ns = g.prof_done_ns = 0;
     for (auto &t : g.prof_thread) t = Lib::ThreadProf{};

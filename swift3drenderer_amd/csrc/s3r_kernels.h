@@ -16,13 +16,16 @@ namespace s3r {
 // write nothing -- the host fills them (launch_sky_flags) -- and neither do the row chunks of covered
 // bins that end without a winner:
 // each bin's workgroup stores chunk_flags[bin] = (fill_tag << 32) | mask at its end, bit
-// (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.
+// (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.  stage (with
+// frame_rows and host_fill; device address of a 3 W H byte host buffer): every other chunk that lies
+// wholly inside the frame is stored there packed at 3 bytes a pixel (frame row y at stage + 3 W y,
+// little-endian b, g, r) instead of into out, for the host to widen (complete before the mask).
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
                      bool frame_rows = false, uint32_t host_fill = 0, unsigned long long *chunk_flags = nullptr,
-                     uint32_t fill_tag = 0, bool row_starts = false);
+                     uint32_t fill_tag = 0, bool row_starts = false, uint8_t *stage = nullptr);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
 // pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0

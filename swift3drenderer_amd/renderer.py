@@ -138,8 +138,8 @@ class Renderer:
         return {'frames': int(out[0]), 'pre_us': us(out[1]), 'issued_us': us(out[2]), 'dev_end_us': us(out[3]),
                 'fill_end_us': us(out[4]), 'joined_us': us(out[5]), 'placed': bool(out[6]),
                 'node': ctypes.c_int64(out[7]).value,
-                'threads': [{'cpu': int(out[8 + 4 * t]), 'end_us': us(out[9 + 4 * t]), 'px': int(out[10 + 4 * t] // f)}
-                            for t in range(n)]}
+                'threads': [{'cpu': int(out[8 + 4 * t]), 'end_us': us(out[9 + 4 * t]), 'px': int(out[10 + 4 * t] // f),
+                             'covered_us': us(out[11 + 4 * t])} for t in range(n)]}
 
     def tile_stats(self) -> dict:
         """Tile path list sizing (include/render.h s3r_tile_stats)."""
