@@ -64,10 +64,11 @@ int main() {
     CK(hipHostRegister(stage, sbytes, hipHostRegisterPortable | hipHostRegisterMapped));
     unsigned *sdev;
     CK(hipHostGetDevicePointer((void **)&sdev, stage, 0));
-    uint32_t *frame = (uint32_t *)aligned_alloc(4096, (npx * 4 + 4095) & ~(size_t)4095);
+    uint32_t *frame = (uint32_t *)aligned_alloc(4096, (npx * 4 + 64 + 4095) & ~(size_t)4095);
     memset(frame, 0, npx * 4);
     auto doms = domains();
     const int T = 4;
+    size_t piece = 64;
     auto run_widen = [&](const char *what) {
         auto t0 = std::chrono::steady_clock::now();
         std::vector<std::thread> th;
@@ -77,11 +78,12 @@ int main() {
                 for (int c : doms[(size_t)t % doms.size()]) CPU_SET(c, &set);
                 pthread_setaffinity_np(pthread_self(), sizeof set, &set);
             }
-            // chunk-sized pieces (64 px), in an order that jumps between rows like bins do
-            const size_t chunks = npx / 64;
+            // pieces of `piece` pixels (a chunk, or a bin's row of 6 chunks), in an order that jumps
+            // between rows like bins do; the frame 16 B into its first line, as a malloc'd buffer
+            const size_t chunks = npx / piece - 1;
             for (size_t k = t; k < chunks; k += T) {
                 const size_t c = (k * 2654435761ull) % chunks;
-                widen(stage + 3 * 64 * c, frame + 64 * c, 64);
+                widen(stage + 3 * piece * c, frame + 4 + piece * c, piece);
             }
             _mm_sfence();
         });
@@ -89,12 +91,16 @@ int main() {
         printf("%-40s %8.1f us\n", what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     };
     (void)W;
-    for (int rep = 0; rep < 3; rep++) {
-        memset(stage, rep, npx * 3);
-        run_widen("widen, staging written by the CPU");
-        hipLaunchKernelGGL(k_stage, dim3(1024), dim3(256), 0, nullptr, sdev, npx * 3 / 4, (unsigned)rep);
-        CK(hipDeviceSynchronize());
-        run_widen("widen, staging written by the GPU");
+    for (size_t pc : {64, 384}) {
+        piece = pc;
+        printf("pieces of %zu px\n", pc);
+        for (int rep = 0; rep < 2; rep++) {
+            memset(stage, rep, npx * 3);
+            run_widen("widen, staging written by the CPU");
+            hipLaunchKernelGGL(k_stage, dim3(1024), dim3(256), 0, nullptr, sdev, npx * 3 / 4, (unsigned)rep);
+            CK(hipDeviceSynchronize());
+            run_widen("widen, staging written by the GPU");
+        }
     }
     return 0;
 }
