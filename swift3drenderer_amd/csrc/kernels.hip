@@ -2084,11 +2084,12 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
     const float4 *__restrict__ nrm, const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
     const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
     float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
-    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local) {
+    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows) {
     const uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
     const uint32_t lr = blockIdx.y * 4u + (threadIdx.x >> 6);
     if (x >= W || lr >= rows_local) return;
     const size_t idx = (size_t)lr * W + x;
+    const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
     const unsigned long long k = keys[idx];
     uint32_t v = kBackground;
     if (k) {
@@ -2097,7 +2098,6 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
         const float4 *q = reinterpret_cast<const float4 *>(recs + s);
         const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
         const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
-        const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
         const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
         const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
         const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
@@ -2130,7 +2130,7 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
         }
         v = shade(&ts, w0, w1, w2, ooz, tex, ntex);
     }
-    out[idx] = v;
+    out[frame_rows ? (size_t)y * W + x : idx] = v;      // (frame_rows: the caller's mapped frame)
 }
 
 // ------------------------------------------------------------------ self-test kernel
@@ -2480,11 +2480,11 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st) {
+                         uint32_t rows_local, hipStream_t st, bool frame_rows) {
     if (W == 0 || rows_local == 0) return;
     hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64, (rows_local + 3) / 4), dim3(256), 0, st, keys,
                        (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex, ntex,
-                       out, W, band, nparts, part, rows_local);
+                       out, W, band, nparts, part, rows_local, frame_rows ? 1u : 0u);
 }
 
 }  // namespace s3r

@@ -131,6 +131,7 @@ struct Dev {
     bool tile_pending = false;
     uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
     uint32_t *tile_out = nullptr;
+    bool tile_frame_rows = false;
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
@@ -758,8 +759,11 @@ bool use_tile_path() {
 
 // The tile path's fill and fragment stage of buffer set p (its setup done): scatter into the set's
 // list (capacity d.tile_list_cap[p]), raster, resolve into out, on st after the geometry stream.
+// frame_rows: out is the whole W x H frame (the caller's mapped buffer; direct delivery), each local
+// row stored at its frame row.
 void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, uint32_t *out, hipStream_t geo, hipStream_t st, TimingSlot *ts) {
+                         uint32_t rows_local, uint32_t *out, hipStream_t geo, hipStream_t st, TimingSlot *ts,
+                         bool frame_rows) {
     const float sw = (float)W, sh = (float)d.tile_H;
     launch_tile_fill(d.boxes[p], g.ntri, d.recs[p], d.app_list[p], d.app_count[p], W, band, nparts, part,
                      d.tile_cursor[p], d.tile_list[p], d.tile_list_cap[p], geo);
@@ -770,7 +774,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p], d.tile_list[p],
                        d.keys, d.tile_total[p], d.tile_list_cap[p], st);
     launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st);
+                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());
@@ -802,13 +806,13 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     hipStream_t geo = d.geo[0];
     launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_total[p], geo);
     tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
-                        nullptr);
+                        nullptr, d.tile_frame_rows);
     HIPCHECK(hipStreamSynchronize(st));
     return true;
 }
 
 void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                  uint32_t *out, hipStream_t st, TimingSlot *ts, bool sync) {
+                  uint32_t *out, hipStream_t st, TimingSlot *ts, bool sync, bool frame_rows) {
     if (W > 65535 || H > 65535) {                       // packed 16-bit bboxes
         fprintf(stderr, "s3r: tile path supports frames up to 65535 x 65535\n");
         exit(1);
@@ -881,7 +885,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         d.tile_readbacks++;
         grow_tile_list(d, p, host[1]);
     }
-    tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts);
+    tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts, frame_rows);
     if (sync) {
         // this frame's totals to the host, for the overflow check once the frame is done
         HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -889,6 +893,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         d.tile_pending_set = p;
         d.tile_W = W; d.tile_band = band; d.tile_nparts = nparts; d.tile_part = part; d.tile_rows = rows_local;
         d.tile_out = out;
+        d.tile_frame_rows = frame_rows;
     }
 }
 
@@ -907,8 +912,9 @@ struct HostFill {
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
 // band split (nparts = 1, band = H: the whole frame) into `out` on `st`, asynchronously.  With hf
-// (row path only) `out` is the whole W x H frame in the caller's mapped host buffer: the fragment
-// kernel writes this part's bins at their frame rows -- only the covered ones for host fill.
+// `out` is the whole W x H frame in the caller's mapped host buffer: the fragment kernel writes this
+// part's bins at their frame rows -- only the covered ones for host fill (row path only; the tile
+// path's resolve writes every pixel of the part at its frame row, direct delivery).
 //
 // sync (updateAndRender's frames, waited for before the call returns): the geometry runs on `st`
 // itself -- nothing could overlap it, and stream order replaces the cross-stream event (~9 us per
@@ -918,7 +924,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
                  uint32_t *out, hipStream_t st, const HostFill *hf = nullptr, bool sync = false) {
     TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
-        render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts, sync);
+        render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts, sync, hf != nullptr);
         return;
     }
     d.last_path = 1;
@@ -1618,6 +1624,8 @@ void deliver_part_direct(void *arg, int i) {
     if (i == 0)
         job.issued_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     HIPCHECK(hipStreamSynchronize(d.stream));
+    // a tile-path frame whose list overflowed is rendered again, into the same rows
+    if (fp.rows_local && job.W) tile_redo_if_overflowed(d, d.stream);
     note_end(job, job.dev_end_ns);
 }
 
@@ -1802,10 +1810,10 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     bool pinned = false;
     if (copy_bytes) pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
     const int mode = delivery_mode();
-    if (pinned && npx && copy_bytes == frame_bytes && mode != kCopy && !use_tile_path()) {
+    if (pinned && npx && copy_bytes == frame_bytes && mode != kCopy) {
         // direct / host fill: the GPU(s) write straight into the buffer (host fill: covered bins only,
-        // the sky bins by the host)
-        const bool fill = mode == kFill || mode == kAuto;
+        // the sky bins by the host; the tile path delivers direct -- its resolve writes every pixel)
+        const bool fill = (mode == kFill || mode == kAuto) && !use_tile_path();
         const MappedResult mr = g.unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, nparts, fill);
         if (mr == kMapped) {
             g.pinned_frames++;

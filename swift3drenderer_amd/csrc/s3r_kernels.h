@@ -116,7 +116,7 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st);
+                         uint32_t rows_local, hipStream_t st, bool frame_rows = false);
 
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);

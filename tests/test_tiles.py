@@ -193,3 +193,41 @@ def test_sync_frames_without_list_readback(gpu_renderer, icosa_dir, monkeypatch)
         assert st['overflows'] > 0 and st['readbacks'] <= 4 + st['overflows'], st
     finally:
         r.set_raster_path('auto')
+
+
+@pytest.mark.parametrize('mode', ['copy', 'direct', 'auto'])
+@pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
+def test_tile_deliveries_match_oracle(gpu_renderer, icosa_dir, monkeypatch, mode, devices):
+    """Tile-path frames (the stress scene) delivered by copy, or written by the resolve kernel straight
+    into their rows of the caller's buffer (direct; 'auto' picks it, host fill being a row-path
+    delivery) -- on one device and three parts, into the halves of a double buffer, with frames whose
+    list overflowed (S3R_TILE_LIST_EXACT=1) rendered again into the same rows."""
+    from oracle.oracle import OracleRenderer
+    monkeypatch.setenv('S3R_TILE_LIST_EXACT', '1')
+    r = gpu_renderer
+    r.configure_devices(devices)
+    path = icosa_dir[2000]
+    r.configure(path)
+    r.set_delivery(mode)
+    try:
+        o = OracleRenderer(path)
+        seq = ([(640, 480, (0, 0, 0, 0, 0, 0))] + [(640, 480, (40.0, 0, 0, 0, 0.0, 0.0))] * 10 +
+               [(1280, 720, (0, 0, 0, 0, 25.0, -10.0))] * 3)
+        mem, cur = None, 0
+        for k, (w, h, inp) in enumerate(seq):
+            if mem is None or mem.size != 2 * w * h:
+                mem, cur = np.empty(2 * w * h, dtype=np.uint32), 0
+            half = mem[cur * w * h:(cur + 1) * w * h].reshape(h, w)
+            cur ^= 1
+            half[:] = 0x5A5A5A5A
+            got = r.update_and_render(w, h, inp, half)
+            want = o.update_and_render(w, h, inp)
+            assert np.array_equal(got, want), f'frame {k} {w}x{h}: ' + diff(got, want)
+        assert r.raster_path() == 'tiles'
+        st = r.host_stats()
+        used = 'copy' if mode == 'copy' else 'direct'
+        assert st[f'{used}_frames'] == len(seq) and st['pinned_frames'] == len(seq), st
+        assert r.tile_stats()['overflows'] > 0, r.tile_stats()
+    finally:
+        r.set_delivery('env')
+        r.configure_devices([])
