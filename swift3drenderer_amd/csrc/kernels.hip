@@ -886,6 +886,89 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     return res;
 }
 
+#ifndef S3R_SHADE_PK
+#define S3R_SHADE_PK 0
+#endif
+// shade_core_flat with the independent f32 chains paired into v_pk_{mul,add,fma}_f32 (two lanes per
+// instruction; the same IEEE operations, so the same bits): the quotients w0, w1 / (1/z), the texture
+// coordinates (u, v) and their level quotients, the position and normal interpolations and their
+// normalisations side by side (P in the low halves, N in the high), the colour's (r, g).  For the
+// waterfall shading, whose constants sit in SGPRs: each packed source is an SGPR pair or a broadcast.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v pdiv_recip(f2v b) {
+    const f2v r = {S3R_RCP(b.x), S3R_RCP(b.y)};
+    return pfma(pfma(-b, r, (f2v){1.0f, 1.0f}), r, r);
+}
+__device__ __forceinline__ f2v pdiv_with_recip(f2v a, f2v b, f2v r) {
+    const f2v q0 = a * r;
+    const f2v q1 = pfma(pfma(-b, q0, a), r, q0);
+    return pfma(pfma(-b, q1, a), r, q1);
+}
+__device__ __forceinline__ f2v psqrt_in_range(f2v x) {
+    const f2v s = {S3R_SQRT(x.x), S3R_SQRT(x.y)};
+    const u2v su = __builtin_bit_cast(u2v, s);
+    const f2v sm = __builtin_bit_cast(f2v, su - 1u), sp = __builtin_bit_cast(f2v, su + 1u);
+    const f2v rm = pfma(-sm, s, x), rp = pfma(-sp, s, x);
+    const float tx = rm.x <= 0.0f ? sm.x : s.x, ty = rm.y <= 0.0f ? sm.y : s.y;
+    return (f2v){rp.x > 0.0f ? sp.x : tx, rp.y > 0.0f ? sp.y : ty};
+}
+S3R_CALLEE uint32_t shade_core_pk(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0,
+                                  float4 k1, float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1,
+                                  float w2, float ooz, const uint32_t *__restrict__ tex, uint32_t ntex) {
+    auto inr = [](float x) { return (fabsf(x) >= 0x1p-40f) & (fabsf(x) < 0x1p20f); };
+    bool ok = inr(w0) & inr(w1) & inr(w2) & inr(ooz);
+    const float r = div_recip(ooz);
+    const f2v oo = {ooz, ooz}, rr = {r, r};
+    const f2v ab = pdiv_with_recip((f2v){w0, w1}, oo, rr);
+    const float a = ab.x, b = ab.y, c = div_with_recip(w2, ooz, r);
+    // texture coordinates first: the texel load overlaps the normalisations
+    const f2v muv = ((f2v){k0.x, k0.y} * a + (f2v){k0.z, k0.w} * b) + (f2v){k1.x, k1.y} * c;
+    const f2v dvv = (f2v){k2.x, k2.y} - muv * (f2v){k1.z, k1.w};
+    const f2v dv = {fabsf(dvv.x), fabsf(dvv.y)};
+    const bool texd = kind != kColour;
+    ok &= !texd | (inr(dv.x) & inr(dv.y));
+    const f2v lv = pdiv_with_recip(oo, dv, pdiv_recip(dv));
+    const bool tex_ok = texd & (tex_base < ntex) & (ntex - tex_base >= kTexTexels);
+    uint32_t rgb = tex[tex_ok ? tex_base + texel_offset(muv.x, muv.y, lv.x, lv.y) : 0u];
+    // (P, N) side by side: X = (P.x, N.x), ...
+    const f2v X = ((f2v){c0.x, n0.x} * a + (f2v){c1.x, n1.x} * b) + (f2v){c2.x, n2.x} * c;
+    const f2v Y = ((f2v){c0.y, n0.y} * a + (f2v){c1.y, n1.y} * b) + (f2v){c2.y, n2.y} * c;
+    const f2v Z = ((f2v){c0.z, n0.z} * a + (f2v){c1.z, n1.z} * b) + (f2v){c2.z, n2.z} * c;
+    const f2v d = (X * X + Y * Y) + Z * Z;                                            // simd_dot
+    ok &= sqrt_in_range_ok(d.x) & sqrt_in_range_ok(d.y);
+    const f2v sq = psqrt_in_range(d);
+    const f2v inv = pdiv_with_recip((f2v){1.0f, 1.0f}, sq, pdiv_recip(sq));
+    const f2v nx = X * inv, ny = Y * inv, nz = Z * inv;           // (pn, normal) components
+    // halfway = normalize(-pn + normal); s = dot(halfway, normal)
+    const F3 h = mk3(-nx.x + nx.y, -ny.x + ny.y, -nz.x + nz.y);
+    const float hd = dot3(h, h);
+    ok &= sqrt_in_range_ok(hd);
+    const float hs = sqrt_in_range(hd);
+    const float hinv = div_with_recip(1.0f, hs, div_recip(hs));
+    const F3 hw = mk3(h.x * hinv, h.y * hinv, h.z * hinv);
+    float s = dot3(hw, mk3(nx.y, ny.y, nz.y));
+    asm volatile("" : "+v"(rgb), "+v"(s));
+    rgb = tex_ok ? rgb : 0u;
+    f2v cxy;
+    float cz;
+    if (texd) {
+        cxy = (f2v){(float)(rgb >> 16), (float)((rgb >> 8) & 255u)};
+        cz = (float)(rgb & 255u);
+    } else {
+        cxy = ((f2v){k0.x, k0.y} * a + (f2v){k1.x, k1.y} * b) + (f2v){k2.x, k2.y} * c;
+        cz = (k0.z * a + k1.z * b) + k2.z * c;
+    }
+    const f2v sc = cxy * s;
+    uint32_t res = rgb_pack(sc.x, sc.y, s * cz);
+    if (!ok) {
+        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(ooz));
+        res = shade_core<false>(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, w0, w1, w2, ooz, tex, ntex);
+    }
+    return res;
+}
+
 // The same from a TriSetup record (tile path: a register-resident record).
 S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
                           const uint32_t *__restrict__ tex, uint32_t ntex) {
@@ -1444,8 +1527,13 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                     const bool mine = act && wp == wu;
                     todo &= ~__ballot(mine);
                     if (mine)
+#if S3R_SHADE_PK
+                        px = shade_core_pk(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
+                                           depth[p], tex, ntex);
+#else
                         px = shade_core_flat(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
                                              depth[p], tex, ntex);
+#endif
                 }
                 if (packed) {
                     put_packed(cx0, px);
