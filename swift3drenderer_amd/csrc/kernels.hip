@@ -1963,10 +1963,10 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ counts,
     const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, const uint32_t *__restrict__ total,
-    uint32_t cap) {
+    uint32_t cap, uint32_t tile0) {
     __shared__ TileShared ls;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t tile = blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const uint32_t tile = tile0 + blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t lx0 = tx * kTileW, lx1 = min(W, lx0 + kTileW) - 1u;
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
     auto row_of = [&](uint32_t lr) { return nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band; };
@@ -2172,9 +2172,9 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
     const float4 *__restrict__ nrm, const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
     const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
     float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
-    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows) {
+    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows, uint32_t by0) {
     const uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
-    const uint32_t lr = blockIdx.y * 4u + (threadIdx.x >> 6);
+    const uint32_t lr = (by0 + blockIdx.y) * 4u + (threadIdx.x >> 6);
     if (x >= W || lr >= rows_local) return;
     const size_t idx = (size_t)lr * W + x;
     const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
@@ -2499,6 +2499,8 @@ void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, u
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
+uint32_t tile_height() { return kTileH; }
+static_assert(kTileH % 4u == 0, "tile rows = whole 4-row resolve blocks (slabbed fragment stage)");
 uint32_t tile_count(uint32_t W, uint32_t rows_local) { return tile_grid_x(W) * ((rows_local + kTileH - 1) / kTileH); }
 uint64_t tile_slots(uint32_t W, uint32_t rows_local) { return (uint64_t)tile_count(W, rows_local) * kDepthBuckets; }
 
@@ -2556,23 +2558,26 @@ void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, co
 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st) {
-    const uint32_t nt = tile_count(W, rows_local);
-    if (nt == 0) return;
-    hipLaunchKernelGGL(k_tile_raster, dim3(nt), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band, nparts,
-                       part, rows_local, tile_grid_x(W), offs, counts, list, keys, total,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
+                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st,
+                        uint32_t ty0, uint32_t ty1) {
+    const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
+    ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
+    if (tx == 0 || ty0 >= ty1) return;
+    hipLaunchKernelGGL(k_tile_raster, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
+                       band, nparts, part, rows_local, tx, offs, counts, list, keys, total,
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx);
 }
 
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows) {
-    if (W == 0 || rows_local == 0) return;
-    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64, (rows_local + 3) / 4), dim3(256), 0, st, keys,
+                         uint32_t rows_local, hipStream_t st, bool frame_rows, uint32_t r0, uint32_t r1) {
+    r1 = std::min(r1, rows_local);
+    if (W == 0 || r0 >= r1 || (r0 & 3u)) return;
+    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64, (r1 - r0 + 3) / 4), dim3(256), 0, st, keys,
                        (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex, ntex,
-                       out, W, band, nparts, part, rows_local, frame_rows ? 1u : 0u);
+                       out, W, band, nparts, part, r1, frame_rows ? 1u : 0u, r0 / 4u);
 }
 
 }  // namespace s3r

@@ -96,6 +96,8 @@ struct HostProf {
 };
 
 // One GPU: its replica of the scene, its per-frame buffer sets, streams and frame tags.
+constexpr uint32_t kMaxTileSlabs = 16;
+
 struct Dev {
     int device = -1;
     float4 *vtx = nullptr, *nrm = nullptr, *pay = nullptr;
@@ -136,6 +138,11 @@ struct Dev {
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
+    // tile path with direct delivery: the fragment stage in row slabs, slab k's resolve (its stores
+    // cross the link) on res_stream while slab k + 1 rasterizes on the frame's stream (created on
+    // first use)
+    hipStream_t res_stream = nullptr;
+    hipEvent_t slab_done[kMaxTileSlabs] = {}, res_done = nullptr;
     // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
     // fragment launch (complete by stream order) in *done_host (host-coherent memory; done_dev is its
     // device address); issued_tag[p] = the tag of the last fragment launch that read set p (0: none);
@@ -304,6 +311,7 @@ struct Lib {
     uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
     uint64_t nindices = 0;
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
+    uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -548,6 +556,10 @@ void initialize() {
         g.band = e && atoi(e) > 0 ? (uint32_t)atoi(e) : kDefaultBand;
     }
     g.serial = getenv("S3R_SERIAL") != nullptr;
+    {
+        const char *e = getenv("S3R_TILE_SLABS");
+        g.tile_slabs = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
+    }
     for (int id : ids) {
         Dev *d = new Dev();
         d->device = id;
@@ -602,6 +614,10 @@ void dev_release(Dev &d) {
     }
     for (hipStream_t gs : d.geo)
         if (gs) (void)hipStreamDestroy(gs);
+    for (hipEvent_t e : d.slab_done)
+        if (e) (void)hipEventDestroy(e);
+    if (d.res_done) (void)hipEventDestroy(d.res_done);
+    if (d.res_stream) (void)hipStreamDestroy(d.res_stream);
     for (auto &t : d.tslots) {
         (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
     }
@@ -771,10 +787,38 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     follow_previous_frame(d, st);
     HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p], d.tile_list[p],
-                       d.keys, d.tile_total[p], d.tile_list_cap[p], st);
-    launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                        d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows);
+    // Direct delivery in row slabs (S3R_TILE_SLABS = k > 1; whole tile rows): slab i's resolve, whose
+    // stores cross the link, on res_stream after slab i's raster, overlapping slab i + 1's raster on
+    // st; st joins res_stream at the end (the next frame's raster overwrites the keys).  Measured on
+    // the 4K stress frame: 1 slab 552-554 fps, 2: 483, 4: 461-463, 8: 407 -- off by default.
+    const uint32_t th = tile_height(), tyn = (rows_local + th - 1) / th;
+    uint32_t slabs = frame_rows ? g.tile_slabs : 1u;
+    slabs = std::max(1u, std::min({slabs, tyn, kMaxTileSlabs}));
+    if (slabs == 1u) {
+        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p],
+                           d.tile_list[p], d.keys, d.tile_total[p], d.tile_list_cap[p], st);
+        launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
+                            sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows);
+    } else {
+        if (!d.res_stream) {
+            HIPCHECK(hipSetDevice(d.device));
+            HIPCHECK(hipStreamCreateWithFlags(&d.res_stream, hipStreamNonBlocking));
+            for (hipEvent_t &e : d.slab_done) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&d.res_done, hipEventDisableTiming));
+        }
+        for (uint32_t k = 0; k < slabs; k++) {
+            const uint32_t ty0 = (uint32_t)((uint64_t)tyn * k / slabs), ty1 = (uint32_t)((uint64_t)tyn * (k + 1) / slabs);
+            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p],
+                               d.tile_list[p], d.keys, d.tile_total[p], d.tile_list_cap[p], st, ty0, ty1);
+            HIPCHECK(hipEventRecord(d.slab_done[k], st));
+            HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
+            launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
+                                sw, sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.res_stream, frame_rows,
+                                ty0 * th, std::min(rows_local, ty1 * th));
+        }
+        HIPCHECK(hipEventRecord(d.res_done, d.res_stream));
+        HIPCHECK(hipStreamWaitEvent(st, d.res_done, 0));
+    }
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());

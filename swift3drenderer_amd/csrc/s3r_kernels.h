@@ -88,6 +88,7 @@ void fragment_configure(uint32_t W, uint32_t rows_local);
 // recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts / offs / cursor:
 // tile_slots() (tile, bucket) entries; scan_temp: tile_scan_temp_bytes(tile_slots()) bytes.
 uint32_t tile_count(uint32_t W, uint32_t rows_local);
+uint32_t tile_height();                        // rows of a tile (a multiple of the resolve's 4-row blocks)
 uint64_t tile_slots(uint32_t W, uint32_t rows_local);
 size_t tile_scan_temp_bytes(uint64_t nslots);
 size_t raster_rec_bytes();
@@ -111,12 +112,14 @@ void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, co
 // keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st);
+                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st,
+                        uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu);   // tile rows [ty0, ty1) only
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows = false);
+                         uint32_t rows_local, hipStream_t st, bool frame_rows = false,
+                         uint32_t r0 = 0, uint32_t r1 = 0xFFFFFFFFu);     // local rows [r0, r1) only (r0 % 4 == 0)
 
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);
