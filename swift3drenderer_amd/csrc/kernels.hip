@@ -2173,11 +2173,17 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
     const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
     float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
     uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows, uint32_t by0) {
-    const uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
     const uint32_t lr = (by0 + blockIdx.y) * 4u + (threadIdx.x >> 6);
-    if (x >= W || lr >= rows_local) return;
-    const size_t idx = (size_t)lr * W + x;
+    if (lr >= rows_local) return;
     const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
+    // frame_rows == 2 (the caller's mapped frame, uncached registration): each wave's 64 pixels start
+    // on the 64-B line grid of the caller's row -- a row of a malloc'd buffer begins rsh pixels into a
+    // line, so the wave takes pixels [64 bx - rsh, 64 bx - rsh + 64) (one block more per row) and its
+    // store crosses the link as four whole lines instead of five partly written ones
+    uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
+    if (frame_rows == 2u) x -= (uint32_t)(((uintptr_t)(out + (size_t)y * W)) >> 2) & 15u;
+    if (x >= W) return;                                // (x wrapped below 0 included)
+    const size_t idx = (size_t)lr * W + x;
     const unsigned long long k = keys[idx];
     uint32_t v = kBackground;
     if (k) {
@@ -2572,12 +2578,14 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows, uint32_t r0, uint32_t r1) {
+                         uint32_t rows_local, hipStream_t st, bool frame_rows, uint32_t r0, uint32_t r1,
+                         bool line_grid) {
     r1 = std::min(r1, rows_local);
     if (W == 0 || r0 >= r1 || (r0 & 3u)) return;
-    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64, (r1 - r0 + 3) / 4), dim3(256), 0, st, keys,
-                       (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex, ntex,
-                       out, W, band, nparts, part, r1, frame_rows ? 1u : 0u, r0 / 4u);
+    const uint32_t mode = frame_rows ? (line_grid ? 2u : 1u) : 0u;
+    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64 + (mode == 2u ? 1u : 0u), (r1 - r0 + 3) / 4), dim3(256), 0,
+                       st, keys, (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex,
+                       ntex, out, W, band, nparts, part, r1, mode, r0 / 4u);
 }
 
 }  // namespace s3r

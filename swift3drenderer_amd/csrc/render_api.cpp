@@ -312,6 +312,7 @@ struct Lib {
     uint64_t nindices = 0;
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
+    bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -559,6 +560,8 @@ void initialize() {
     {
         const char *e = getenv("S3R_TILE_SLABS");
         g.tile_slabs = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
+        const char *l = getenv("S3R_TILE_LINE");
+        g.tile_line_grid = !(l && atoi(l) == 0);
     }
     for (int id : ids) {
         Dev *d = new Dev();
@@ -798,7 +801,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
         launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p],
                            d.tile_list[p], d.keys, d.tile_total[p], d.tile_list_cap[p], st);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
-                            sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows);
+                            sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
+                            g.tile_line_grid);
     } else {
         if (!d.res_stream) {
             HIPCHECK(hipSetDevice(d.device));
@@ -814,7 +818,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
             HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
             launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
                                 sw, sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.res_stream, frame_rows,
-                                ty0 * th, std::min(rows_local, ty1 * th));
+                                ty0 * th, std::min(rows_local, ty1 * th), g.tile_line_grid);
         }
         HIPCHECK(hipEventRecord(d.res_done, d.res_stream));
         HIPCHECK(hipStreamWaitEvent(st, d.res_done, 0));

@@ -119,7 +119,8 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                          uint32_t rows_local, hipStream_t st, bool frame_rows = false,
-                         uint32_t r0 = 0, uint32_t r1 = 0xFFFFFFFFu);     // local rows [r0, r1) only (r0 % 4 == 0)
+                         uint32_t r0 = 0, uint32_t r1 = 0xFFFFFFFFu,      // local rows [r0, r1) only (r0 % 4 == 0)
+                         bool line_grid = false);   // frame_rows: wave stores on the caller's 64-B line grid
 
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);

@@ -233,14 +233,18 @@ def test_tile_deliveries_match_oracle(gpu_renderer, icosa_dir, monkeypatch, mode
         r.configure_devices([])
 
 
+@pytest.mark.parametrize('line', ['1', '0'])
 @pytest.mark.parametrize('slabs', ['1', '3', '16'])
 @pytest.mark.parametrize('devices', [[0], [0, 0]])
-def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, devices):
+def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, devices, line):
     """Direct tile-path frames rendered in row slabs (S3R_TILE_SLABS: slab k's resolve on a second
     stream while slab k + 1 rasterizes) equal the oracle's, for slab counts that divide the tile rows
-    unevenly or exceed them, frame heights that end inside a tile, and two parts."""
+    unevenly or exceed them, frame heights that end inside a tile, and two parts; with the resolve's
+    waves on the caller's 64-B line grid (S3R_TILE_LINE=1, the default: rows starting mid-line, an
+    odd width) and without."""
     from oracle.oracle import OracleRenderer
     monkeypatch.setenv('S3R_TILE_SLABS', slabs)
+    monkeypatch.setenv('S3R_TILE_LINE', line)
     r = gpu_renderer
     r.configure_devices(devices)
     path = icosa_dir[2000]
@@ -249,7 +253,8 @@ def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, de
     try:
         o = OracleRenderer(path)
         seq = ([(640, 483, (0, 0, 0, 0, 0, 0))] + [(640, 483, (40.0, 0, 0, 0, 0.0, 0.0))] * 4 +
-               [(1280, 720, (0, 0, 0, 0, 25.0, -10.0))] * 2 + [(96, 37, (0, 0, 0, 0, 0.0, 0.0))])
+               [(1280, 720, (0, 0, 0, 0, 25.0, -10.0))] * 2 + [(96, 37, (0, 0, 0, 0, 0.0, 0.0))] +
+               [(333, 77, (0, 0, 0, 0, 0.0, 0.0))])
         for k, (w, h, inp) in enumerate(seq):
             out = np.full((h, w), 0x5A5A5A5A, dtype=np.uint32)
             got = r.update_and_render(w, h, inp, out)
