@@ -166,8 +166,23 @@ void s3r_scene_counts(uint64_t out[8]);
 /* Tile path (device 0): out[0] frames whose tile-list size was read back before the fill (one host
  * sync: asynchronous frames and each buffer set's first), out[1] synchronous updateAndRender frames
  * whose list, sized by earlier frames, overflowed and that were rendered again, out[2] the last
- * frame's (tile, triangle) pairs, out[3] 0. */
+ * frame's (tile, triangle) pairs, out[3] the live slots (meeting this part's rows) of the last
+ * frame whose counters were read back. */
 void s3r_tile_stats(uint64_t out[4]);
+
+/* Tile path clusters (built at load for scenes the tile path renders, clusters.cpp): out[0] the
+ * cluster count (0: none), out[1] 1 when the tile path culls them (S3R_CLUSTERS != 0), out[2] the
+ * triangles of the clusters the last read-back frame kept, out[3] 1 when the setup order is a
+ * permutation of the file order.  Extension: replaces nothing in render.cpp (render.cpp:297 visits
+ * every triangle). */
+void s3r_cluster_stats(uint64_t out[4]);
+
+/* Test hook, no GPU needed: the clusters the library builds for a vertex list (nv x float4) and
+ * index list (3 ntri vertex indices < nv).  Returns the cluster count C; writes the first
+ * min(C + 1, first_cap) position-range starts to first_out, min(C, first_cap) bounding spheres
+ * (centre xyz, radius) to sphere_out and, when perm_out is not null, the ntri slots in cluster order. */
+uint32_t s3r_build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_t ntri, uint32_t *first_out,
+                            float *sphere_out, uint32_t first_cap, uint32_t *perm_out);
 
 /* Copy the current camera matrix (3 rows x 4) and raster factor. */
 void s3r_camera(float out_matrix[12], float *out_factor);

@@ -29,7 +29,7 @@ FLAGS = ['-O3', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-ffp-contract=
          '-fno-fast-math', '-Wall', '-Wno-unused-function', '-Wno-bitwise-instead-of-logical', f'-I{os.path.join(ROOT, "include")}']
 SOURCES = ['kernels.hip', 'render_api.cpp']
 # host-only C++ (no HIP): compiled by g++ so x86 intrinsics stay out of the HIP compilation
-HOST_SOURCES = ['host_fill.cpp']
+HOST_SOURCES = ['host_fill.cpp', 'clusters.cpp']
 HOST_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-Wall']
 
 

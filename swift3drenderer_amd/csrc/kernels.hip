@@ -20,6 +20,9 @@
 #include "s3r_kernels.h"
 
 #include <hip/hip_ext.h>
+
+#include <map>
+#include <mutex>
 #include <rocprim/device/device_scan.hpp>
 
 namespace s3r {
@@ -1803,117 +1806,288 @@ __global__ void __launch_bounds__(256) k_tile_vertex(const float4 *__restrict__ 
     rv[i] = make_float4(d.rv.x, d.rv.y, d.rv.z, 0.0f);
 }
 
-template <bool VS>
-__global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
-                                                    uint32_t ntri, Mat34 m, float factor, float sw, float sh,
-                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
-                                                    RasterRec *__restrict__ recs, uint32_t *__restrict__ boxes,
-                                                    uint32_t *__restrict__ app_list, uint32_t *__restrict__ app_count,
-                                                    uint32_t *__restrict__ counts, const float4 *__restrict__ vrv) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool in = t < ntri;
-    const float half_w = sw / 2, half_h = sh / 2;
-    Vert d[3];
-    TriSetup ts;
-    bool live = false;
-    if (in) {
-        uint32_t vi[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            vi[k] = vidx[3 * t + k];
-            if (VS) {
-                const float4 r = vrv[vi[k]];                                   // the vertex stage's rv
-                d[k].rv = mk3(r.x, r.y, r.z);
-                d[k].cv = mk3(0, 0, 0);
-            } else {
-                load_corner(vtx, vi[k], m, factor, half_w, half_h, d[k]);
-            }
-            d[k].n = mk3(0, 0, 0);
-            d[k].pay = make_float4(0, 0, 0, 0);
-        }
-        if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
-            if (fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear) {               // :308, rare
-                if (VS) {                         // the clip needs camera-space corners: recompute
-#pragma unroll
-                    for (int k = 0; k < 3; k++) load_corner(vtx, vi[k], m, factor, half_w, half_h, d[k]);
-                }
-                Vert app[3];
-                uint32_t app_first = 0;
-                // positions do not depend on the colour / texture payload (clip's `textured`)
-                if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) {
-                    TriSetup ta;
-                    if (raster_part(app, sw, sh, ta)) {
-                        const uint32_t zba = f2u(ooz_bound(ta));
-                        const TileSpan sa = box_tiles(tile_box(ta.xmin | (ta.xmax << 16), zba), ta.ymin | (ta.ymax << 16),
-                                                      band, nparts, part);
-                        if (sa.n) {                     // only triangles meeting this part's rows
-                            write_rec(recs + ntri + t, ta, ntri + t, zba);
-                            app_list[atomicAdd(app_count, 1u)] = ntri + t;
-                        }
-                        for (uint32_t k = 0; k < sa.n; k++)
-                            atomicAdd(&counts[((sa.ty0 + k / sa.ntx) * tiles_x + sa.tx0 + k % sa.ntx) * kDepthBuckets +
-                                              sa.bucket], 1u);
-                    }
-                }
-            }
-            live = raster_part(d, sw, sh, ts);
-        }
+// Sharded streams.  The cluster cull, the setup and the fill work on per-shard lists: a workgroup b
+// serves shard b % kTileShards, so appends are wave-aggregated atomics on kTileShards separate
+// counters (one cache line apart) -- device-scope atomics on ONE address serialise at ~8-11 ns each
+// (measured: one shared counter made the 20 M-triangle setup 2.4 ms), distinct addresses proceed in
+// parallel.  Shard s owns the positions [base(s), base(s + 1)) (with clusters: the triangles of its
+// clusters, a static table, cmap holding the kept ones; without: an even split of the slots), the
+// live entries [2 base(s), 2 base(s + 1)) (a slot and its clip-appended slot) and the clip queue
+// [base(s), base(s + 1)).  Counters: 0 positions kept, 1 live entries, 2 clip queue.
+__device__ __forceinline__ uint32_t *shard_ctr(uint32_t *ctr, uint32_t which, uint32_t s) {
+    return ctr + kTileCounterWords * 16u + (which * kTileShards + s) * kTileShardStride;
+}
+__device__ __forceinline__ uint32_t shard_base(const uint32_t *tab, uint32_t ntri, uint32_t s) {
+    return tab ? tab[s] : (uint32_t)((uint64_t)s * ntri / kTileShards);
+}
+
+// Wave-aggregated append of one entry per lane with `want` to list (counter *n): one atomic per wave.
+__device__ __forceinline__ void wave_append(bool want, uint4 e, uint4 *__restrict__ list, uint32_t *__restrict__ n) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const uint32_t lane = threadIdx.x & 63u, leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    if (want) list[base + lane_prefix(m, lane)] = e;
+}
+
+// Cluster cull (clusters.cpp): can any triangle of the cluster in sphere s (world centre, radius)
+// give this part a raster record?  No when every vertex lies behind the near plane (render.cpp:306
+// rejects each triangle), when the sphere's screen box lies off one side of the frame (:312-314), or
+// when its rows miss the part's interleaved bands.  Conservative: the camera-space centre carries a
+// float error far below E, and the screen box is widened by a pixel; a sphere reaching the near
+// plane is kept (clipped triangles, :308).
+__device__ __forceinline__ bool cluster_meets(float4 s, const Mat34 &m, float factor, float sw, float sh, uint32_t band,
+                                              uint32_t nparts, uint32_t part) {
+    if (!(s.w < __builtin_inff())) return true;
+    const F3 c = mat_mul(m, make_float4(s.x, s.y, s.z, 1.0f));
+    const float E = 1e-5f * (fabsf(s.x) + fabsf(s.y) + fabsf(s.z) + fabsf(m.m[0][3]) + fabsf(m.m[1][3]) +
+                             fabsf(m.m[2][3]) + s.w);
+    const float r = s.w + E, nz = -c.z;
+    if (nz + r < kNear) return false;                           // every vertex behind the near plane
+    const float z0 = nz - r, z1 = nz + r;
+    if (!(z0 > 2.0f * kNear)) return true;                      // reaches the near plane: no bound
+    // screen x = cv.x f / nz + W/2, y = -cv.y f / nz + H/2 (render.cpp:288) over the sphere
+    const float ax = c.x - r, bx = c.x + r, ay = -c.y - r, by = -c.y + r;
+    const float xlo = (ax < 0 ? ax / z0 : ax / z1) * factor + sw / 2, xhi = (bx > 0 ? bx / z0 : bx / z1) * factor + sw / 2;
+    const float ylo = (ay < 0 ? ay / z0 : ay / z1) * factor + sh / 2, yhi = (by > 0 ? by / z0 : by / z1) * factor + sh / 2;
+    const float mx = 1.0f + 1e-5f * (fabsf(xlo) + fabsf(xhi)), my = 1.0f + 1e-5f * (fabsf(ylo) + fabsf(yhi));
+    if (xhi + mx < 0 || yhi + my < 0 || xlo - mx >= sw || ylo - my >= sh) return false;   // off screen
+    if (nparts == 1u) return true;
+    const uint32_t y0 = u32_of_float(fmaxf(0.0f, ylo - my)), y1 = u32_of_float(fminf(sh - 1, yhi + my));
+    uint32_t lo, hi;
+    return local_row_range(y0, y1, band, nparts, part, lo, hi);
+}
+
+// One thread per cluster (workgroup b: clusters 256 b ..., shard b % kTileShards): the surviving
+// clusters' triangle positions, appended to their shard's part of cmap.
+__global__ void __launch_bounds__(256) k_cluster_cull(const float4 *__restrict__ sphere, const uint32_t *__restrict__ first,
+                                                      uint32_t ncl, const uint32_t *__restrict__ shard_tab, Mat34 m,
+                                                      float factor, float sw, float sh, uint32_t band, uint32_t nparts,
+                                                      uint32_t part, uint32_t *__restrict__ cmap, uint32_t *__restrict__ ctr) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards;
+    uint32_t n = 0, f0 = 0;
+    if (i < ncl && cluster_meets(sphere[i], m, factor, sw, sh, band, nparts, part)) {
+        f0 = first[i];
+        n = first[i + 1] - f0;
     }
+    uint32_t inc = n;                                           // wave prefix sum of the sizes
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+        if (lane >= o) inc += v;
+    }
+    const uint32_t tot = (uint32_t)__shfl((int)inc, 63);
+    if (tot == 0) return;
+    uint32_t base = 0;
+    if (lane == 63u) base = atomicAdd(shard_ctr(ctr, 0, sh_id), tot);
+    base = (uint32_t)__shfl((int)base, 63) + shard_tab[sh_id];
+    // the wave's kept positions, written coalesced: output o comes from the first lane whose
+    // inclusive prefix exceeds o (binary search over the prefixes by lane shuffles)
+    for (uint32_t o0 = 0; o0 < tot; o0 += 64u) {
+        const uint32_t o = o0 + lane;
+        uint32_t L = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1u; step >>= 1)
+            if ((uint32_t)__shfl((int)inc, (int)(L + step - 1u)) <= o) L += step;
+        L = min(L, 63u);
+        const uint32_t fL = (uint32_t)__shfl((int)f0, (int)L), exL = (uint32_t)__shfl((int)(inc - n), (int)L);
+        if (o < tot) cmap[base + o] = fL + (o - exL);
+    }
+}
+
+// u32 flavour of wave_append (the clip queue)
+__device__ __forceinline__ void wave_append_u32(bool want, uint32_t v, uint32_t *__restrict__ list, uint32_t *__restrict__ n) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const uint32_t lane = threadIdx.x & 63u, leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    if (want) list[base + lane_prefix(m, lane)] = v;
+}
+
+// A live slot's raster record, live entry and (tile, bucket) counts -- or nothing when its box misses
+// this part's rows (row-band split: the slot is dead here).  Every lane of the wave calls it (the
+// entry append and the counting are wave-aggregated).
+__device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_t slot, uint32_t band, uint32_t nparts,
+                                          uint32_t part, uint32_t tiles_x, RasterRec *__restrict__ recs,
+                                          uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
+                                          uint32_t *__restrict__ counts) {
     uint32_t bx = kDeadBox, by = 0;
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
         const uint32_t zb = f2u(ooz_bound(ts));
         const uint32_t bt = tile_box(ts.xmin | (ts.xmax << 16), zb);
         sp = box_tiles(bt, ts.ymin | (ts.ymax << 16), band, nparts, part);
-        // a triangle outside this part's rows (row-band split) is dead here: no record, no box
         if (sp.n) {
             bx = bt;
             by = ts.ymin | (ts.ymax << 16);
-            write_rec(recs + t, ts, t, zb);
+            write_rec(recs + slot, ts, slot, zb);
         }
     }
-    if (in) reinterpret_cast<uint2 *>(boxes)[t] = make_uint2(bx, by);
+    wave_append(bx != kDeadBox, make_uint4(bx, by, slot, 0), lv, nlive);
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 1)
     if (bx == 12345u)                                   // ablation: no tile counting
 #endif
     tile_visit(sp, tiles_x, counts, nullptr, 0);
 }
 
-// After the exclusive scan of the (tile, bucket) counts (rocprim, launch_tile_setup): the fill's
-// scatter cursors start at the offsets, and *total = the list length.
-__global__ void __launch_bounds__(256) k_tile_cursor(const uint32_t *__restrict__ counts, const uint32_t *__restrict__ offs,
-                                                     uint32_t n, uint32_t *__restrict__ cursor, uint32_t *__restrict__ total) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    cursor[i] = offs[i];
-    if (i == n - 1u) *total = offs[i] + counts[i];
+// The slot of position p (cluster order -> file order).
+template <bool CL>
+__device__ __forceinline__ uint32_t slot_of(uint32_t p, const uint32_t *__restrict__ cmap, const uint32_t *__restrict__ cperm) {
+    if (!CL) return p;
+    const uint32_t q = cmap[p];
+    return cperm ? cperm[q] : q;
 }
 
-// Scatter: thread i the original triangle i (packed bbox), then the i-th clip-appended slot if
-// there is one (i < *napp: at most one appended slot per triangle, so the grid covers them).  The
-// list holds cap entries: a frame whose list needs more (sized from an earlier frame, no read-back)
-// writes only those, and the host renders it again with a larger list (render_api.cpp render_tiles).
-__global__ void __launch_bounds__(256) k_tile_fill(const uint32_t *__restrict__ boxes, uint32_t ntri,
-                                                   const RasterRec *__restrict__ recs,
-                                                   const uint32_t *__restrict__ app_list, const uint32_t *__restrict__ napp,
+// Setup, one lane per triangle; workgroup b serves shard s = b % kTileShards, grid-stride over the
+// shard's positions p = base(s) + j (with clusters: the cull's kept positions, slot_of).  A triangle
+// wholly past the near plane is set up here (emit_slot); one that crosses it (render.cpp:308, rare)
+// is queued for k_tile_clip -- the clip keeps it out of this loop's registers (occupancy: the
+// setup is memory-latency-bound).
+template <bool VS, bool CL>
+__global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
+                                                    uint32_t ntri, const uint32_t *__restrict__ cmap,
+                                                    const uint32_t *__restrict__ cperm, const uint32_t *__restrict__ shard_tab,
+                                                    Mat34 m, float factor, float sw, float sh,
+                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
+                                                    RasterRec *__restrict__ recs, uint4 *__restrict__ live,
+                                                    uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
+                                                    uint32_t *__restrict__ counts, const float4 *__restrict__ vrv) {
+    const uint32_t lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards, rank = blockIdx.x / kTileShards;
+    const uint32_t per = gridDim.x / kTileShards;              // workgroups per shard (launch: a multiple)
+    const uint32_t b0 = shard_base(CL ? shard_tab : nullptr, ntri, sh_id);
+    const uint32_t n = CL ? __atomic_load_n(shard_ctr(ctr, 0, sh_id), __ATOMIC_RELAXED)
+                          : shard_base(nullptr, ntri, sh_id + 1) - b0;
+    uint4 *const lv = live + 2ull * b0;
+    uint32_t *const nlive = shard_ctr(ctr, 1, sh_id), *const nclip = shard_ctr(ctr, 2, sh_id);
+    const float half_w = sw / 2, half_h = sh / 2;
+    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += per * 256u) {   // wave-uniform
+        const uint32_t j = j0 + lane;
+        Vert d[3];
+        TriSetup ts;
+        bool live_t = false, clip = false;
+        uint32_t t = 0;
+        if (j < n) {
+            t = slot_of<CL>(b0 + j, cmap, cperm);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const uint32_t vi = vidx[3 * t + k];
+                if (VS) {
+                    const float4 r = vrv[vi];                                      // the vertex stage's rv
+                    d[k].rv = mk3(r.x, r.y, r.z);
+                } else {
+                    load_corner(vtx, vi, m, factor, half_w, half_h, d[k]);
+                }
+            }
+            if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
+                clip = fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear;             // :308, rare
+                if (!clip) live_t = raster_part(d, sw, sh, ts);
+            }
+        }
+        wave_append_u32(clip, b0 + j, clipq + b0, nclip);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
+    }
+}
+
+// The queued triangles that cross the near plane (render.cpp:308-310): clip, then set up the
+// clip-appended slot T + t (if any) and the clipped slot t -- positions only (clip's `textured`
+// affects only the payload).  Workgroup b serves shard b % kTileShards.
+template <bool CL>
+__global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
+                                                   uint32_t ntri, const uint32_t *__restrict__ cmap,
+                                                   const uint32_t *__restrict__ cperm, const uint32_t *__restrict__ shard_tab,
+                                                   Mat34 m, float factor, float sw, float sh,
+                                                   uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
+                                                   RasterRec *__restrict__ recs, uint4 *__restrict__ live,
+                                                   const uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
+                                                   uint32_t *__restrict__ counts) {
+    const uint32_t lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards, rank = blockIdx.x / kTileShards;
+    const uint32_t per = gridDim.x / kTileShards;
+    const uint32_t b0 = shard_base(CL ? shard_tab : nullptr, ntri, sh_id);
+    const uint32_t n = *shard_ctr(ctr, 2, sh_id);
+    uint4 *const lv = live + 2ull * b0;
+    uint32_t *const nlive = shard_ctr(ctr, 1, sh_id);
+    const float half_w = sw / 2, half_h = sh / 2;
+    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += per * 256u) {   // wave-uniform
+        const uint32_t j = j0 + lane;
+        Vert d[3];
+        TriSetup ts, ta;
+        bool live_t = false, live_a = false;
+        uint32_t t = 0;
+        if (j < n) {
+            t = slot_of<CL>(clipq[b0 + j], cmap, cperm);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
+                d[k].n = mk3(0, 0, 0);
+                d[k].pay = make_float4(0, 0, 0, 0);
+            }
+            Vert app[3];
+            uint32_t app_first = 0;
+            if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) live_a = raster_part(app, sw, sh, ta);
+            live_t = raster_part(d, sw, sh, ts);
+        }
+        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
+    }
+}
+
+// After the exclusive scan of the (tile, bucket) counts (rocprim, launch_tile_setup): the fill's
+// scatter cursors start at the offsets.  first (the frame's own launch, not a redo after an
+// overflow): workgroup 0 also writes the summary -- ctr[0] the live entries (summed over the
+// shards), ctr[1] the list length, ctr[2] the positions the cluster cull kept -- and, when sum_host
+// (host-coherent, 4 words) is given, the same three words then the frame's tag into it (system
+// scope, tag last: the host spins on it instead of a stream synchronisation); and every count is
+// reset to 0 for the set's next frame (k_tile_raster reads the offsets only; counts start zeroed).
+__global__ void __launch_bounds__(256) k_tile_cursor(uint32_t *__restrict__ counts, const uint32_t *__restrict__ offs,
+                                                     uint32_t n, uint32_t *__restrict__ cursor, uint32_t *__restrict__ ctr,
+                                                     uint32_t first, uint32_t *__restrict__ sum_host, uint32_t tag) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (first && blockIdx.x == 0 && threadIdx.x < 64u) {
+        static_assert(kTileShards == 64, "one lane per shard");
+        uint32_t kept = *shard_ctr(ctr, 0, threadIdx.x), lv = *shard_ctr(ctr, 1, threadIdx.x);
+        for (int o = 32; o > 0; o >>= 1) {
+            kept += (uint32_t)__shfl_xor((int)kept, o);
+            lv += (uint32_t)__shfl_xor((int)lv, o);
+        }
+        if (threadIdx.x == 0) {
+            const uint32_t total = offs[n - 1u] + counts[n - 1u];
+            if (n - 1u >= 256u) counts[n - 1u] = 0u;       // (its own workgroup leaves it to this one)
+            ctr[0] = lv; ctr[1] = total; ctr[2] = kept;
+            if (sum_host) {
+                __hip_atomic_store(sum_host + 1, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(sum_host + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(sum_host + 3, kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(sum_host, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    if (first && blockIdx.x == 0) __syncthreads();              // (thread 0 has read counts[n - 1])
+    if (i >= n) return;
+    cursor[i] = offs[i];
+    if (first && (i != n - 1u || blockIdx.x == 0)) counts[i] = 0u;
+}
+
+// Scatter: workgroup b serves shard b % kTileShards, grid-stride over its live entries (original and
+// clip-appended slots): each entry's slot into the lists of its tiles.  The list holds cap entries: a
+// frame whose list needs more (sized from an earlier frame, no read-back) writes only those, and the
+// host renders it again with a larger list (render_api.cpp render_tiles).
+__global__ void __launch_bounds__(256) k_tile_fill(const uint4 *__restrict__ live, uint32_t *__restrict__ ctr,
+                                                   const uint32_t *__restrict__ shard_tab, uint32_t ntri,
                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                    uint32_t *__restrict__ cursor, uint32_t *__restrict__ list, uint32_t cap) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, na = *napp;
-    uint32_t bx = kDeadBox, by = 0;
-    if (i < ntri) {
-        const uint2 b = reinterpret_cast<const uint2 *>(boxes)[i];
-        bx = b.x; by = b.y;
+    const uint32_t lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards, rank = blockIdx.x / kTileShards;
+    const uint32_t per = gridDim.x / kTileShards;
+    const uint32_t n = *shard_ctr(ctr, 1, sh_id);
+    const uint4 *const lv = live + 2ull * shard_base(shard_tab, ntri, sh_id);
+    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += per * 256u) {   // wave-uniform
+        const uint32_t j = j0 + lane;
+        uint4 e = make_uint4(kDeadBox, 0, 0, 0);
+        if (j < n) e = lv[j];
+        tile_visit(box_tiles(e.x, e.y, band, nparts, part), tiles_x, cursor, list, e.z, cap);
     }
-    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, i, cap);
-    if (__ballot(i < na) == 0) return;                    // (wave-uniform: no appended slot for this wave)
-    uint32_t slot = 0;
-    bx = kDeadBox; by = 0;
-    if (i < na) {
-        slot = app_list[i];
-        const uint4 h = reinterpret_cast<const uint4 *>(recs + slot)[0];
-        bx = tile_box(h.x, h.w); by = h.y;
-    }
-    tile_visit(box_tiles(bx, by, band, nparts, part), tiles_x, cursor, list, slot, cap);
 }
 
 struct TileShared {
@@ -1972,9 +2146,11 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     auto row_of = [&](uint32_t lr) { return nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band; };
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
     // the tile's list: its depth buckets, nearest first, one after another
-    const uint32_t s0 = tile * kDepthBuckets, sl = s0 + kDepthBuckets - 1u;
+    const uint32_t s0 = tile * kDepthBuckets;
     // a list longer than its buffer (overflow, see k_tile_fill) is incomplete: the frame is redone
-    const uint32_t base = offs[s0], n = *total > cap ? 0u : offs[sl] + counts[sl] - base;
+    const uint32_t ntiles = tiles_x * ((rows_local + kTileH - 1u) / kTileH);
+    const uint32_t end = tile + 1u < ntiles ? offs[s0 + kDepthBuckets] : *total;
+    const uint32_t base = offs[s0], n = *total > cap ? 0u : end - base;
     if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
     // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
     // while stage c0's items run
@@ -2518,47 +2694,102 @@ size_t tile_scan_temp_bytes(uint64_t nslots) {
 }
 size_t raster_rec_bytes() { return sizeof(RasterRec); }
 
+std::vector<uint32_t> cluster_shard_table(const std::vector<uint32_t> &first) {
+    std::vector<uint32_t> tab(kTileShards + 1, 0u);
+    const uint32_t ncl = first.empty() ? 0u : (uint32_t)first.size() - 1;
+    for (uint32_t c = 0; c < ncl; c++) tab[(c / 256u) % kTileShards + 1] += first[c + 1] - first[c];
+    for (uint32_t s = 0; s < kTileShards; s++) tab[s + 1] += tab[s];
+    return tab;
+}
+
+// Grid of a sharded grid-stride kernel: kTileShards x (up to what the whole chip holds resident at
+// once, so every workgroup runs from the start and the shards' loops end together -- a grid larger
+// than that leaves its late workgroups to run all their iterations after the others have finished),
+// fewer when there is less work.
+uint32_t shard_grid(const void *kernel, uint64_t work) {
+    // workgroups per shard: S3R_TILE_GRID = k (k > 0) or 0 (what the device keeps resident); default 128
+    static const int knob = getenv("S3R_TILE_GRID") ? atoi(getenv("S3R_TILE_GRID")) : 128;
+    uint64_t cap = knob > 0 ? (uint64_t)knob : 0;
+    if (!cap) {
+        static std::mutex mu;                      // (device worker threads launch concurrently)
+        static std::map<const void *, uint32_t> resident;   // workgroups of 256 the device keeps resident
+        std::lock_guard<std::mutex> lk(mu);
+        uint32_t &r = resident[kernel];
+        if (!r) {
+            int dev = 0, cus = 0, per_cu = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+            r = std::max(kTileShards, (uint32_t)(std::max(cus, 1) * std::max(per_cu, 1)));
+        }
+        cap = std::max<uint64_t>(1, r / kTileShards);
+    }
+    const uint64_t per = std::min<uint64_t>(cap, std::max<uint64_t>(1, (work / kTileShards + 255) / 256));
+    return (uint32_t)(per * kTileShards);
+}
+template <class K> uint32_t shard_grid(K *kernel, uint64_t work) {
+    return shard_grid(reinterpret_cast<const void *>(kernel), work);
+}
+
+template <bool VS, bool CL>
+void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
+                  float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, void *recs,
+                  uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv, hipStream_t st) {
+    const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
+    hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri)), dim3(256), 0, st, vtx, vidx,
+                       ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq,
+                       ctr, counts, vrv);
+    // the clip queue is short (triangles crossing the near plane): one workgroup per shard
+    hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
+                       factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq, ctr, counts);
+}
+
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                       void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
-                       uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
-                       hipStream_t st, float4 *vrv, uint32_t nv) {
+                       void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
+                       uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
+                       uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag) {
     const uint64_t ns = tile_slots(W, rows_local);
-    (void)hipMemsetAsync(counts, 0, sizeof(uint32_t) * ns, st);
-    (void)hipMemsetAsync(app_count, 0, sizeof(uint32_t), st);
-    if (vrv && nv)
+    (void)hipMemsetAsync(ctr, 0, kTileCtrWords * sizeof(uint32_t), st);      // (counts: zeroed by k_tile_cursor)
+    const bool clustered = cl && cl->ncl;
+    if (vrv && nv && !clustered)
         hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv);
     if (ntri) {
-        if (vrv)
-            hipLaunchKernelGGL(k_tile_setup<true>, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor,
-                               sw, sh, band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count,
-                               counts, (const float4 *)vrv);
-        else
-            hipLaunchKernelGGL(k_tile_setup<false>, dim3((ntri + 255) / 256), dim3(256), 0, st, vtx, vidx, ntri, m, factor,
-                               sw, sh, band, nparts, part, tile_grid_x(W), (RasterRec *)recs, boxes, app_list, app_count,
-                               counts, (const float4 *)nullptr);
+        const uint32_t tx = tile_grid_x(W);
+        if (clustered) {
+            hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
+                               cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr);
+            setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
+                                      ctr, counts, nullptr, st);
+        } else if (vrv) {
+            setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
+                                      ctr, counts, vrv, st);
+        } else {
+            setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live,
+                                       clipq, ctr, counts, nullptr, st);
+        }
     }
     size_t bytes = scan_temp_bytes;
     (void)rocprim::exclusive_scan(scan_temp, bytes, (const uint32_t *)counts, offs, 0u, (size_t)ns,
                                   rocprim::plus<uint32_t>(), st);
     hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
-                       cursor, total);
+                       cursor, ctr, 1u, sum_host, tag);
 }
 
 void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
-                        uint32_t *total, hipStream_t st) {
+                        uint32_t *ctr, hipStream_t st) {
     const uint64_t ns = tile_slots(W, rows_local);
     if (ns == 0) return;
-    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
-                       cursor, total);
+    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, (uint32_t *)counts, offs,
+                       (uint32_t)ns, cursor, ctr, 0u, (uint32_t *)nullptr, 0u);
 }
 
-void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list,
-                      const uint32_t *napp, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor,
-                      uint32_t *list, uint64_t cap, hipStream_t st) {
+void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
+                      uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
+                      hipStream_t st) {
     if (ntri == 0) return;
-    hipLaunchKernelGGL(k_tile_fill, dim3((ntri + 255) / 256), dim3(256), 0, st, boxes, ntri, (const RasterRec *)recs,
-                       app_list, napp, band, nparts, part, tile_grid_x(W), cursor, list,
+    hipLaunchKernelGGL(k_tile_fill, dim3(shard_grid(k_tile_fill, ntri)), dim3(256), 0, st, live, ctr,
+                       cl && cl->ncl ? cl->shard : nullptr, ntri, band, nparts, part, tile_grid_x(W), cursor, list,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
 }
 

@@ -40,6 +40,10 @@
 #include "../../include/render.h"
 #include "s3r_kernels.h"
 
+namespace s3r_host {   // clusters.cpp
+void build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_t ntri, uint32_t kmin, uint32_t kmax,
+                    std::vector<uint32_t> &first, std::vector<float> &sphere, std::vector<uint32_t> &perm);
+}
 namespace s3r_host {   // host_fill.cpp
 void fill_words(uint32_t *p, size_t n, uint32_t v);
 void widen_pixels(const uint8_t *src, uint32_t *dst, size_t n);
@@ -71,6 +75,9 @@ constexpr int kSets = 4;
 #endif
 constexpr int kGeoStreams = S3R_GEO_STREAMS;
 constexpr uint64_t kLptMinBins = 4000;      // longest-first fragment order from this many bins (~3 rounds; see render_core)
+// Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
+// the order-independent tile path takes over (the icosahedron stress scene).
+constexpr uint64_t kRowPathMaxSlots = 8192;
 constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
 constexpr int kMaxDevices = 64;
 
@@ -122,12 +129,19 @@ struct Dev {
     size_t scan_temp_bytes = 0;
     float4 *vrv = nullptr;                     // tile path vertex stage (S3R_VERTEX_STAGE): projected vertices
     void *recs[kSets] = {};        // 2T raster records (positions-only setup)
-    uint32_t *boxes[kSets] = {};   // T packed bboxes
-    uint32_t *app_list[kSets] = {}, *app_count[kSets] = {};
+    uint4 *live[kSets] = {};       // 2T live entries (tile box, rows, slot), per shard
+    uint32_t *clipq = nullptr;     // T: positions whose triangle crosses the near plane (one: setups run on geo[0])
+    uint32_t *tile_ctr[kSets] = {};  // kTileCounterWords: live count, list total, cluster-kept triangles
+    // init-time clusters (clusters.cpp): spheres, position ranges, position -> slot (null: identity),
+    // and the cull's per-frame position list (one: every tile-path setup runs on geo[0])
+    float4 *cl_sphere = nullptr;
+    uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_map = nullptr, *cl_shard = nullptr;
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
-    uint32_t *tile_total_host = nullptr;       // pinned: (appended, total) per buffer set
+    // host-coherent, per buffer set: {tag, live entries, list length, cluster-kept positions}, written
+    // by k_tile_cursor as soon as they are known (tag = the frame's number)
+    uint32_t *tile_sum_host = nullptr, *tile_sum_dev = nullptr;
     // a synchronous tile-path frame awaiting its overflow check (tile_redo_if_overflowed): its set
     // and what its fragment stage needs to run again
     bool tile_pending = false;
@@ -136,6 +150,7 @@ struct Dev {
     bool tile_frame_rows = false;
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
+    uint64_t last_live = 0, last_kept = 0;     // tile path, last read-back frame: live slots, cluster-kept triangles
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
     // tile path with direct delivery: the fragment stage in row slabs, slab k's resolve (its stores
@@ -182,6 +197,9 @@ struct HostScene {
     std::vector<float4> vtx, nrm, pay;
     std::vector<uint8_t> disc;
     std::vector<uint32_t> vidx, aidx, tex;
+    std::vector<uint32_t> cl_first, cl_perm;   // clusters (tile path): position ranges, position -> slot
+    std::vector<uint32_t> cl_shard;            // where each shard's positions start (cluster_shard_table)
+    std::vector<float> cl_sphere;              // 4 per cluster: centre, radius
 };
 
 // Persistent worker threads, one per device beyond the first: run(fn, arg, n) calls fn(arg, 0) on
@@ -310,6 +328,8 @@ struct Lib {
     // scene counts (the same on every device)
     uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
     uint64_t nindices = 0;
+    uint32_t ncl = 0;                          // clusters (clusters.cpp; 0: the scene has none)
+    bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
@@ -352,11 +372,28 @@ struct Lib {
     uint64_t prof_frames = 0, prof_dev_ns = 0, prof_fill_ns = 0, prof_pre_ns = 0, prof_issued_ns = 0, prof_done_ns = 0;
     std::chrono::steady_clock::time_point call_t0;     // updateAndRender's entry (the profile's pre_ns)
     struct ThreadProf { int64_t cpu = -1; uint64_t end_ns = 0, px = 0, covered_ns = 0; } prof_thread[65];
-    bool unmapped = false;                     // a device could not map a caller buffer: copy only
+    // a device could not map the registration starting at unmapped_a (in registration epoch
+    // unmapped_epoch): frames into it go by copy; other registrations still try the mapping
+    uintptr_t unmapped_a = 0;
+    uint64_t unmapped_epoch = 0;
+    // environment switches read once per library state (release_all resets them: a configure re-reads)
+    int env_row_starts = -1, env_host_uncached = -1;
+    // fill-thread placement: frames in a row whose buffer sat on another node than the placement's
+    int fill_node_streak = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
 };
 
 Lib g;
+
+// A default-on switch from the environment (unset or non-zero: on), cached in `slot` until the
+// library state is reset (s3r_configure / s3r_shutdown).
+bool env_on(int &slot, const char *name) {
+    if (slot < 0) {
+        const char *e = getenv(name);
+        slot = !e || atoi(e) != 0 ? 1 : 0;
+    }
+    return slot == 1;
+}
 
 float config_scale() {
     const float fov = (float)M_PI / 5.f;        // render.cpp:91
@@ -486,6 +523,15 @@ HostScene read_scene() {
     }
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
+    // clusters for the tile path's per-frame cull (scenes the tile path renders by default, or any
+    // scene with S3R_CLUSTERS=1): connected meshes of 8-32 triangles, larger ones cut, smaller pooled
+    const char *ce = getenv("S3R_CLUSTERS");
+    g.clusters = !(ce && atoi(ce) == 0);
+    if (g.clusters && (2 * ntri > kRowPathMaxSlots || (ce && atoi(ce) != 0)))
+        s3r_host::build_clusters(reinterpret_cast<const float *>(s.vtx.data()), (uint32_t)nv, s.vidx.data(),
+                                 (uint32_t)ntri, 8, 32, s.cl_first, s.cl_sphere, s.cl_perm);
+    g.ncl = s.cl_first.empty() ? 0 : (uint32_t)s.cl_first.size() - 1;
+    if (g.ncl) s.cl_shard = cluster_shard_table(s.cl_first);
     return s;
 }
 
@@ -522,6 +568,19 @@ void dev_init(Dev &d, const HostScene &s) {
     HIPCHECK(hipMemcpy(d.vidx, s.vidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d.aidx, s.aidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d.tex, s.tex.data(), (size_t)g.ntex * 4, hipMemcpyHostToDevice));
+    if (g.ncl) {
+        d.cl_sphere = dalloc<float4>(g.ncl);
+        d.cl_first = dalloc<uint32_t>((size_t)g.ncl + 1);
+        d.cl_map = dalloc<uint32_t>(ntri);
+        d.cl_shard = dalloc<uint32_t>(kTileShards + 1);
+        HIPCHECK(hipMemcpy(d.cl_shard, s.cl_shard.data(), (kTileShards + 1) * 4, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(d.cl_sphere, s.cl_sphere.data(), (size_t)g.ncl * 16, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(d.cl_first, s.cl_first.data(), ((size_t)g.ncl + 1) * 4, hipMemcpyHostToDevice));
+        if (!s.cl_perm.empty()) {
+            d.cl_perm = dalloc<uint32_t>(ntri);
+            HIPCHECK(hipMemcpy(d.cl_perm, s.cl_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
+        }
+    }
 }
 
 // "0,1,2" -> {0, 1, 2}; empty on a malformed list.
@@ -597,18 +656,19 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv, d.geo_cnt};
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv, d.geo_cnt,
+                    d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    for (int q = 0; q < kSets; q++) {      // tile_total aliases app_count
+    for (int q = 0; q < kSets; q++) {      // tile_total aliases tile_ctr
         void *set[] = {d.tris[q], d.rowtab[q], d.bincnt[q], d.pairs[q], d.order[q], d.tile_counts[q], d.tile_offs[q],
-                       d.tile_cursor[q], d.tile_list[q], d.recs[q], d.boxes[q], d.app_list[q], d.app_count[q]};
+                       d.tile_cursor[q], d.tile_list[q], d.recs[q], d.live[q], d.tile_ctr[q]};
         for (void *p : set)
             if (p) (void)hipFree(p);
     }
     if (d.done_host) (void)hipHostFree((void *)d.done_host);
     if (d.handoff) (void)hipEventDestroy(d.handoff);
-    if (d.tile_total_host) (void)hipHostFree(d.tile_total_host);
+    if (d.tile_sum_host) (void)hipHostFree(d.tile_sum_host);
     if (d.fill_flags) (void)hipHostFree(d.fill_flags);
     if (d.fill_chunks) (void)hipHostFree(d.fill_chunks);
     for (int p = 0; p < kSets; p++) {
@@ -711,6 +771,7 @@ void restart_tags(Dev &d, uint32_t next_frame_no) {
         if (d.bincnt[p]) HIPCHECK(hipMemset(d.bincnt[p], 0, d.bins_cap * sizeof(uint32_t)));
     HIPCHECK(hipDeviceSynchronize());
     d.frame_no = next_frame_no;
+    if (d.tile_sum_host) memset(d.tile_sum_host, 0, 4 * kSets * sizeof(uint32_t));   // (tags restart)
     for (uint32_t &t : d.issued_tag) t = 0;
     d.last_tag = 0;
     if (d.done_host) __atomic_store_n(d.done_host, 0u, __ATOMIC_RELEASE);
@@ -766,14 +827,16 @@ void wait_all_fragments(Dev &d, hipStream_t geo) {
     for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[q], 0));
 }
 
-// Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
-// the order-independent tile path takes over (the icosahedron stress scene).
-constexpr uint64_t kRowPathMaxSlots = 8192;
 
 bool use_tile_path() {
     if (g.raster_path == 1) return false;
     if (g.raster_path == 2) return true;
     return 2ull * g.ntri > kRowPathMaxSlots;
+}
+
+// The device's clusters as the tile kernels take them (ncl 0: no cull, S3R_CLUSTERS=0 or none built).
+TileClusters tile_clusters(const Dev &d) {
+    return TileClusters{d.cl_sphere, d.cl_first, d.cl_perm, d.cl_shard, g.clusters ? g.ncl : 0u, d.cl_map};
 }
 
 // The tile path's fill and fragment stage of buffer set p (its setup done): scatter into the set's
@@ -784,8 +847,9 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                          uint32_t rows_local, uint32_t *out, hipStream_t geo, hipStream_t st, TimingSlot *ts,
                          bool frame_rows) {
     const float sw = (float)W, sh = (float)d.tile_H;
-    launch_tile_fill(d.boxes[p], g.ntri, d.recs[p], d.app_list[p], d.app_count[p], W, band, nparts, part,
-                     d.tile_cursor[p], d.tile_list[p], d.tile_list_cap[p], geo);
+    const TileClusters cl = tile_clusters(d);
+    launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p], d.tile_list[p],
+                     d.tile_list_cap[p], geo);
     HIPCHECK(hipEventRecord(d.geo_done[p], geo));
     follow_previous_frame(d, st);
     HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
@@ -841,18 +905,21 @@ void grow_tile_list(Dev &d, uint32_t p, uint64_t total) {
 
 // After a synchronous tile-path frame (its stream drained): if its list overflowed the capacity the
 // set had from earlier frames, render its fragment stage again into a list of the right size and
-// return true (the caller redoes its delivery); the totals are in tile_total_host by then.
+// return true (the caller redoes its delivery); the totals are in tile_sum_host by then.
 bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     if (!d.tile_pending) return false;
     d.tile_pending = false;
     const uint32_t p = d.tile_pending_set;
-    const uint64_t total = d.tile_total_host[2 * p + 1];
+    const volatile uint32_t *sum = d.tile_sum_host + 4 * p;
+    const uint64_t total = sum[2];
     d.last_pairs = total;
+    d.last_live = sum[1];
+    d.last_kept = sum[3];
     if (total <= d.tile_list_cap[p]) return false;
     d.tile_overflows++;
     grow_tile_list(d, p, total);
     hipStream_t geo = d.geo[0];
-    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_total[p], geo);
+    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_ctr[p], geo);
     tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
                         nullptr, d.tile_frame_rows);
     HIPCHECK(hipStreamSynchronize(st));
@@ -874,7 +941,11 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
                 if (*q) HIPCHECK(hipFree(*q));
                 *q = dalloc<uint32_t>(nt);
             }
+            // counts start zeroed (each frame's k_tile_cursor leaves them zero); the null-stream
+            // memset does not order the geometry streams, hence the synchronisation
+            HIPCHECK(hipMemset(d.tile_counts[p], 0, nt * sizeof(uint32_t)));
         }
+        HIPCHECK(hipDeviceSynchronize());
         if (d.scan_temp) HIPCHECK(hipFree(d.scan_temp));
         d.scan_temp_bytes = tile_scan_temp_bytes(nt);
         d.scan_temp = dalloc<uint8_t>(d.scan_temp_bytes);
@@ -892,7 +963,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     // for frame parts, where the per-triangle setup is replicated on every device; S3R_VERTEX_STAGE
     // = 0 / 1 forces it
     const char *vs_env = getenv("S3R_VERTEX_STAGE");
-    if (vs_env ? atoi(vs_env) != 0 : nparts > 1) {
+    if (vs_env ? atoi(vs_env) != 0 : nparts > 1 && !(g.clusters && g.ncl)) {
         if (!d.vrv) d.vrv = dalloc<float4>(g.nv);
     } else if (d.vrv) {
         HIPCHECK(hipDeviceSynchronize());
@@ -902,41 +973,57 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (!d.recs[0]) {
         for (int p = 0; p < kSets; p++) {
             d.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
-            d.boxes[p] = dalloc<uint32_t>((size_t)2 * g.ntri);
-            d.app_list[p] = dalloc<uint32_t>(g.ntri);
-            d.app_count[p] = dalloc<uint32_t>(2);          // [0] appended count, [1] tile-pair total
-            d.tile_total[p] = d.app_count[p] + 1;
+            d.live[p] = dalloc<uint4>((size_t)2 * g.ntri);
+            if (!d.clipq) d.clipq = dalloc<uint32_t>(g.ntri);
+            d.tile_ctr[p] = dalloc<uint32_t>(kTileCtrWords);
+            d.tile_total[p] = d.tile_ctr[p] + 1;
         }
-        HIPCHECK(hipHostMalloc((void **)&d.tile_total_host, 2 * kSets * sizeof(uint32_t)));
+        HIPCHECK(hipHostMalloc((void **)&d.tile_sum_host, 4 * kSets * sizeof(uint32_t),
+                               hipHostMallocCoherent | hipHostMallocMapped));
+        memset(d.tile_sum_host, 0, 4 * kSets * sizeof(uint32_t));
+        HIPCHECK(hipHostGetDevicePointer((void **)&d.tile_sum_dev, d.tile_sum_host, 0));
     }
     const uint32_t p = next_set(d);
     hipStream_t geo = d.geo[0];
     HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[p], 0));
     if (g.serial) wait_all_fragments(d, geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
+    const TileClusters cl = tile_clusters(d);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
-                      d.boxes[p], d.app_list[p], d.app_count[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
-                      d.tile_total[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv);
+                      d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
+                      d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + 4 * p, d.frame_no);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are
     // rendered again after the frame if it overflowed (tile_redo_if_overflowed; the fill and raster
     // kernels bound their list accesses).  S3R_TILE_READBACK=1: always read back.
     const bool readback_env = getenv("S3R_TILE_READBACK") && atoi(getenv("S3R_TILE_READBACK")) != 0;
-    uint32_t *host = d.tile_total_host + 2 * p;
+    volatile uint32_t *sum = d.tile_sum_host + 4 * p;
     d.last_path = 2;
     d.tile_H = H;
     if (!sync || d.tile_list_cap[p] == 0 || readback_env) {
-        HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, geo));
-        HIPCHECK(hipStreamSynchronize(geo));
-        d.last_pairs = host[1];
+        // spin on the summary k_tile_cursor publishes (a stream synchronisation's wake-up costs ~10-20
+        // us a frame); after 2 ms fall back to synchronising, which also surfaces a device fault
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 1; __atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no; k++) {
+            __builtin_ia32_pause();
+            if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                HIPCHECK(hipStreamSynchronize(geo));
+                if (__atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no) {
+                    fprintf(stderr, "s3r: tile path: the frame's summary never arrived\n");
+                    abort();
+                }
+            }
+        }
+        d.last_pairs = sum[2];
+        d.last_live = sum[1];
+        d.last_kept = sum[3];
         d.tile_readbacks++;
-        grow_tile_list(d, p, host[1]);
+        grow_tile_list(d, p, sum[2]);
     }
     tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts, frame_rows);
     if (sync) {
-        // this frame's totals to the host, for the overflow check once the frame is done
-        HIPCHECK(hipMemcpyAsync(host, d.app_count[p], 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        // the overflow check reads this frame's summary once the frame is done
         d.tile_pending = true;
         d.tile_pending_set = p;
         d.tile_W = W; d.tile_band = band; d.tile_nparts = nparts; d.tile_part = part; d.tile_rows = rows_local;
@@ -1038,8 +1125,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     // pair reservations are in (one extra workgroup waits for them on per-row-block counters)
     // delivered frames: the geometry tabulates row starts only, the fragment workgroups walk along
     // their rows themselves (kernels.hip k_geometry); S3R_ROW_STARTS=0: the full start table
-    static const bool row_starts_env = !getenv("S3R_ROW_STARTS") || atoi(getenv("S3R_ROW_STARTS")) != 0;
-    const bool row_starts = hf != nullptr && row_starts_env;
+    const bool row_starts = hf != nullptr && env_on(g.env_row_starts, "S3R_ROW_STARTS");
     GeoSkyFlags gsf{};
     if (hf && hf->flags_dev) {
         if (!d.geo_cnt) {
@@ -1128,8 +1214,7 @@ bool host_pinned(void *p, size_t n) {
     // link then carries whole 64-B lines (54.0 vs 52.0 GB/s for a malloc + 16-B buffer,
     // tools/micro/pcie_write.hip); S3R_HOST_UNCACHED=0 registers it as before.  A runtime that
     // refuses the flag gets the plain registration.
-    static const bool uncached = !getenv("S3R_HOST_UNCACHED") || atoi(getenv("S3R_HOST_UNCACHED")) != 0;
-    bool ok = uncached && hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped |
+    bool ok = env_on(g.env_host_uncached, "S3R_HOST_UNCACHED") && hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped |
                                                                 hipExtHostRegisterUncached) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
@@ -1610,8 +1695,11 @@ void fill_worker(void *arg, int idx) {
         if (keep == n) {
             __builtin_ia32_pause();
             if ((++idle & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
-                fprintf(stderr, "s3r: host fill: %zu bins never flagged (device fault?)\n", keep);
-                abort();
+                // a device that never published these bins (a fault surfaces in the device part's
+                // stream synchronisation): give up on the frame -- it is redone by copy
+                fprintf(stderr, "s3r: host fill: %zu bins never flagged in 20 s; frame redone by copy\n", keep);
+                job.stale.store(true, std::memory_order_relaxed);
+                break;
             }
         }
         n = keep;
@@ -1724,10 +1812,15 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
         g.fill_gpu = g.fill_gpu < 0 ? 0 : (g.fill_gpu > 8 ? 8 : g.fill_gpu);
     }
     if (fill) {
-        // (re)start the fill threads, placed for this buffer's memory node, when the thread count or
-        // the node changes
+        // (re)start the fill threads, placed for this buffer's memory node, when the thread count
+        // changes, or when the buffer has sat on another node for kNodeStreak frames in a row (the two
+        // halves of a double buffer on different nodes must not re-place them every frame: a
+        // placement samples the CPUs' load for 10 ms)
+        constexpr int kNodeStreak = 16;
         const int node = page_node(buffer);
-        if (g.fill_pool.workers() != job.threads || node != g.fill_node) {
+        g.fill_node_streak = node == g.fill_node ? 0 : g.fill_node_streak + 1;
+        if (g.fill_pool.workers() != job.threads || g.fill_node_streak >= kNodeStreak) {
+            g.fill_node_streak = 0;
             const std::vector<cpu_set_t> cpus = fill_placement(job.threads, node);
             g.fill_pool.start(job.threads, cpus.empty() ? nullptr : &cpus);
             g.fill_node = node;
@@ -1862,7 +1955,9 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
         // direct / host fill: the GPU(s) write straight into the buffer (host fill: covered bins only,
         // the sky bins by the host; the tile path delivers direct -- its resolve writes every pixel)
         const bool fill = (mode == kFill || mode == kAuto) && !use_tile_path();
-        const MappedResult mr = g.unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, nparts, fill);
+        const Lib::Reg *reg = find_reg(pixel_data->buffer, frame_bytes);
+        const bool unmapped = reg && g.unmapped_epoch == g.reg_epoch && g.unmapped_a == reg->a;
+        const MappedResult mr = unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, nparts, fill);
         if (mr == kMapped) {
             g.pinned_frames++;
             for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
@@ -1874,9 +1969,11 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
             drop_registration(pixel_data->buffer, pixel_data->bufferSize);
             g.stale_pins++;
             pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
-        } else if (!g.unmapped) {
-            g.unmapped = true;        // a device cannot address the buffer: copy from now on
-            fprintf(stderr, "s3r: a device has no mapping of the caller's buffer; delivering by copy\n");
+        } else if (!unmapped && reg) {
+            // a device cannot address this registration: its frames go by copy
+            g.unmapped_a = reg->a;
+            g.unmapped_epoch = g.reg_epoch;
+            fprintf(stderr, "s3r: a device has no mapping of the caller's buffer; delivering it by copy\n");
         }
     }
     if (copy_bytes) {
@@ -2101,7 +2198,15 @@ __attribute__((visibility("default"))) void s3r_tile_stats(uint64_t out[4]) {
     out[0] = d ? d->tile_readbacks : 0;      // frames whose list size was read back before the fill
     out[1] = d ? d->tile_overflows : 0;      // synchronous frames rendered again into a larger list
     out[2] = d ? d->last_pairs : 0;
-    out[3] = 0;
+    out[3] = d ? d->last_live : 0;           // live slots (meeting this part's rows), last read-back frame
+}
+
+__attribute__((visibility("default"))) void s3r_cluster_stats(uint64_t out[4]) {
+    const Dev *d = g.devs.empty() ? nullptr : g.devs[0];
+    out[0] = g.ncl;                          // clusters built at load (0: none)
+    out[1] = g.clusters && g.ncl ? 1 : 0;    // the tile path culls them (S3R_CLUSTERS)
+    out[2] = d ? d->last_kept : 0;           // triangles of the clusters kept, last read-back frame
+    out[3] = d && d->cl_perm ? 1 : 0;        // positions are a permutation (not the file order)
 }
 
 __attribute__((visibility("default"))) void s3r_camera(float out_matrix[12], float *out_factor) {

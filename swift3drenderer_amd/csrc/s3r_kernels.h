@@ -2,6 +2,8 @@
 #pragma once
 #include "s3r_common.h"
 
+#include <vector>
+
 namespace s3r {
 
 // `done` (may be null): recorded on `st` when the launched kernel completes.
@@ -85,30 +87,55 @@ void fragment_configure(uint32_t W, uint32_t rows_local);
 
 // Tile path (order-independent fragment stage for many triangles): tiles of 16 local rows x 64 px,
 // each tile's list split into depth buckets (nearest first; kernels.hip depth_bucket).
-// recs: 2T x raster_rec_bytes(); boxes: T x 8 B; app_list: T x u32; counts / offs / cursor:
-// tile_slots() (tile, bucket) entries; scan_temp: tile_scan_temp_bytes(tile_slots()) bytes.
+// recs: 2T x raster_rec_bytes(); counts / offs / cursor: tile_slots() (tile, bucket) entries;
+// scan_temp: tile_scan_temp_bytes(tile_slots()) bytes.
 uint32_t tile_count(uint32_t W, uint32_t rows_local);
 uint32_t tile_height();                        // rows of a tile (a multiple of the resolve's 4-row blocks)
 uint64_t tile_slots(uint32_t W, uint32_t rows_local);
 size_t tile_scan_temp_bytes(uint64_t nslots);
 size_t raster_rec_bytes();
+// Init-time clusters (clusters.cpp) on the device: ncl bounding spheres (world centre, radius),
+// first[ncl + 1] position ranges, perm (position -> slot; null: identity), shard[kTileShards + 1]
+// (cluster_shard_table: where each shard's positions start) and cmap, a per-frame scratch of ntri
+// words (the surviving clusters' positions, per shard).
+struct TileClusters {
+    const float4 *sphere;
+    const uint32_t *first, *perm, *shard;
+    uint32_t ncl;
+    uint32_t *cmap;
+};
+// The cull, setup and fill append to kTileShards per-shard lists (kernels.hip "sharded streams");
+// cluster c is culled by workgroup c / 256, which serves shard (c / 256) % kTileShards.
+constexpr uint32_t kTileShards = 64, kTileShardStride = 64;
+// Shard s's first position: the triangles of the clusters of shards < s (kTileShards + 1 entries).
+std::vector<uint32_t> cluster_shard_table(const std::vector<uint32_t> &first);
+// ctr: kTileCtrWords device words per frame (zeroed by launch_tile_setup): [0] live entries, [1] the
+// tile lists' total length, [2] positions the cluster cull kept (the first kTileCounterWords are
+// the summary the host reads back), then the shards' counters.  live: 2T entries (tile box, rows,
+// slot, 0); clipq: T words (the positions whose triangle crosses the near plane).  cl (may be null
+// or empty): cull clusters first and set up only their triangles; vrv (nv float4, may be null;
+// unused with clusters): run the vertex stage first (k_tile_vertex) and set triangles up from its
+// projected vertices.  counts must be zero on entry (allocate them zeroed): the launch leaves them
+// zero again.  sum_host (host-coherent, mapped; may be null): {tag, ctr[0], ctr[1], ctr[2]} written
+// by the device as soon as the summary is known, the tag last (system scope).
+constexpr uint32_t kTileCounterWords = 4;
+constexpr uint32_t kTileCtrWords = kTileCounterWords * 16 + 3 * kTileShards * kTileShardStride;
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-                       void *recs, uint32_t *boxes, uint32_t *app_list, uint32_t *app_count, uint32_t *counts,
-                       uint32_t *offs, uint32_t *cursor, uint32_t *total, void *scan_temp, size_t scan_temp_bytes,
-                       hipStream_t st, float4 *vrv = nullptr, uint32_t nv = 0);
-// vrv (nv float4, may be null): run the vertex stage first (k_tile_vertex) and set triangles up
-// from its projected vertices.
-// napp: device word, the appended slots' count (app_list's length); list: cap entries -- a frame whose
-// list (*total entries, device word) needs more writes only cap of them, and k_tile_raster then
-// renders no triangle (the caller renders the frame again with a larger list).
+                       void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
+                       uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st,
+                       float4 *vrv = nullptr, uint32_t nv = 0, const TileClusters *cl = nullptr,
+                       uint32_t *sum_host = nullptr, uint32_t tag = 0);
+// list: cap entries -- a frame whose list (ctr[1] entries) needs more writes only cap of them, and
+// k_tile_raster then renders no triangle (the caller renders the frame again with a larger list).
 // The fill's scatter cursors reset to the offsets (as launch_tile_setup leaves them): a frame's fill
 // again, e.g. into a larger list after an overflow.
 void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
-                        uint32_t *total, hipStream_t st);
-void launch_tile_fill(const uint32_t *boxes, uint32_t ntri, const void *recs, const uint32_t *app_list,
-                      const uint32_t *napp, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor,
-                      uint32_t *list, uint64_t cap, hipStream_t st);
+                        uint32_t *ctr, hipStream_t st);
+// The same cl as the setup's (it says where the shards' live entries start).
+void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
+                      uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
+                      hipStream_t st);
 // keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,

@@ -77,6 +77,9 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_fill_profile.restype = ctypes.c_uint32
     lib.s3r_tile_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_tile_stats.restype = None
+    if hasattr(lib, 's3r_cluster_stats'):         # (optional: A/B runs load earlier builds via S3R_LIB)
+        lib.s3r_cluster_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+        lib.s3r_cluster_stats.restype = None
     missing = [name for name in EXPORTS if not hasattr(lib, name)]
     if missing:
         raise RuntimeError(f'{path} does not export {missing}: rebuild it (__graft_entry__.build())')
@@ -145,7 +148,15 @@ class Renderer:
         """Tile path list sizing (include/render.h s3r_tile_stats)."""
         out = (ctypes.c_uint64 * 4)()
         self.lib.s3r_tile_stats(out)
-        return {'readbacks': int(out[0]), 'overflows': int(out[1]), 'last_pairs': int(out[2])}
+        return {'readbacks': int(out[0]), 'overflows': int(out[1]), 'last_pairs': int(out[2]),
+                'last_live': int(out[3])}
+
+    def cluster_stats(self) -> dict:
+        """Tile path clusters (include/render.h s3r_cluster_stats)."""
+        out = (ctypes.c_uint64 * 4)()
+        self.lib.s3r_cluster_stats(out)
+        return {'clusters': int(out[0]), 'culling': bool(out[1]), 'last_kept': int(out[2]),
+                'permuted': bool(out[3])}
 
     DELIVERIES = {'env': -1, 'auto': 0, 'copy': 1, 'direct': 2, 'fill': 3}
 

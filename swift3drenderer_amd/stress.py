@@ -185,7 +185,35 @@ def write_stress(path: str, n: int, seed: int = 1) -> int:
     return total
 
 
-_NAME = re.compile(r'^icosa-(stress|\d+)$')
+def write_soup(path: str, n: int, seed: int = 1) -> int:
+    """The n-icosahedron scene as a triangle soup: the same triangles (geometry, normals, colours),
+    but every triangle with its own three vertices (no index shared, so no mesh to find) and the
+    triangles in a shuffled order (SplitMix64 keys, sorted).  Exercises the tile path's pooled,
+    permuted clusters (clusters.cpp); small n only (built in memory)."""
+    v, nrm = _chunk(seed, 0, n)
+    f = np.array(ICOSA_FACES)
+    tv = v[:, f].reshape(-1, 3, 3)                             # (20 n, 3 corners, xyz)
+    cols = _colour_table()
+    rec = np.zeros((n, 20, 3, 12), dtype=F)
+    rec[..., 0:3] = nrm[:, :, None, :]
+    rec[..., 4:8] = cols[None]
+    rec = rec.reshape(-1, 3, 12)
+    order = np.argsort(_splitmix(np.arange(20 * n, dtype=np.uint64) + np.uint64(seed) * GOLDEN), kind='stable')
+    tv, rec = tv[order], rec[order]
+    nt = 20 * n
+    v4 = np.ones((nt, 3, 4), dtype=F)
+    v4[..., :3] = tv
+    hdr = lambda k: np.array([k, 0], dtype=np.uint64).tobytes()     # noqa: E731
+    idx = np.arange(3 * nt, dtype=np.int64)
+    pad = bytes(8) if (3 * nt) % 2 else b''
+    data = b''.join([hdr(3 * nt), v4.tobytes(), hdr(3 * nt), idx.tobytes(), pad, hdr(3 * nt), rec.tobytes(),
+                     hdr(3 * nt), idx.tobytes(), pad, hdr(0)])
+    with open(path, 'wb') as fo:
+        fo.write(data)
+    return len(data)
+
+
+_NAME = re.compile(r'^icosa-(soup-)?(stress|\d+)$')
 
 
 def is_stress_name(name: str) -> bool:
@@ -196,10 +224,12 @@ def count_of(name: str) -> int:
     m = _NAME.match(name)
     if not m:
         raise ValueError(name)
-    return 1_000_000 if m.group(1) == 'stress' else int(m.group(1))
+    return 1_000_000 if m.group(2) == 'stress' else int(m.group(2))
 
 
 def write_named(name: str, path: str) -> int:
+    if _NAME.match(name).group(1):
+        return write_soup(path, count_of(name), seed=1)
     return write_stress(path, count_of(name), seed=1)
 
 

@@ -28,7 +28,16 @@ def icosa_dir(tmp_path_factory):
         p = str(d / f'icosa-{n}.bin')
         stress.write_stress(p, n, seed=1)
         out[n] = p
+    p = str(d / 'icosa-soup-2000.bin')
+    stress.write_soup(p, 2000, seed=1)
+    out['soup'] = p
     return out
+
+
+@pytest.fixture(scope='module')
+def oracle_100k_4k(icosa_dir):
+    """The oracle's 3840x2160 P_id frame of 100 000 icosahedra (shared by the tests below)."""
+    return oracle_render_pose(icosa_dir[100000], poses.script('P_id'), 3840, 2160)
 
 
 def diff(a, b):
@@ -69,13 +78,90 @@ def test_stress_small_matches_oracle(gpu_renderer, icosa_dir, pose, w, h):
     assert np.array_equal(got, want), diff(got, want)
 
 
-def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir):
-    """100 000 icosahedra (2 M triangles) at 3840x2160 -- a tenth of config 5, oracle-checkable."""
+@pytest.mark.parametrize('clusters', ['1', '0'])
+def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir, oracle_100k_4k, monkeypatch, clusters):
+    """100 000 icosahedra (2 M triangles) at 3840x2160 -- a tenth of config 5, oracle-checkable --
+    with the cluster cull (the default) and without (S3R_CLUSTERS=0)."""
+    monkeypatch.setenv('S3R_CLUSTERS', clusters)
     path = icosa_dir[100000]
-    script = poses.script('P_id')
-    want = oracle_render_pose(path, script, 3840, 2160)
-    got = render_pose(gpu_renderer, path, script, 3840, 2160)
+    want = oracle_100k_4k
+    got = render_pose(gpu_renderer, path, poses.script('P_id'), 3840, 2160)
     assert (want != 0x1E1E1E).mean() > 0.9            # the view is filled
+    assert np.array_equal(got, want), diff(got, want)
+    assert gpu_renderer.cluster_stats()['clusters'] == (100000 if clusters == '1' else 0)
+
+
+@pytest.mark.parametrize('nparts', [8, 3])
+def test_stress_100k_4k_parts_match_oracle(gpu_renderer, icosa_dir, oracle_100k_4k, nparts):
+    """One rank's share of an N-GPU split of 100 000 icosahedra at 4K, every part rendered with the
+    cluster cull (each part sets up only the clusters that reach its 16-row bands) and reassembled:
+    the oracle's frame.  The cull must keep far fewer triangles per part than the whole frame's."""
+    import torch
+    from swift3drenderer_amd.multi import assemble
+    W, H, band = 3840, 2160, 16
+    r = gpu_renderer
+    r.configure(icosa_dir[100000])
+    try:
+        script = poses.script('P_id')
+        for t in script:
+            r.update_and_render(W, H, t)
+        inp = (0, 0, 0, 0) + tuple(script[-1][4:6])
+        parts, kept = [], []
+        for part in range(nparts):
+            rows = r.lib.s3r_band_rows_local(H, band, nparts, part)
+            buf = torch.empty((rows, W), dtype=torch.int32, device='cuda')
+            r.render_bands(inp, W, H, band, nparts, part, buf.data_ptr(), 0)
+            torch.cuda.synchronize()
+            parts.append(buf.cpu().numpy().view(np.uint32))
+            kept.append(r.cluster_stats()['last_kept'])
+        got = assemble(parts, H, band)
+        assert np.array_equal(got, oracle_100k_4k), diff(got, oracle_100k_4k)
+        ntri = 20 * 100000
+        # a part owns 16 of every 16 N rows; an icosahedron spans ~17-27 rows
+        assert max(kept) < (0.45 if nparts == 8 else 0.97) * ntri, kept
+        assert min(kept) > 0.1 * ntri, kept
+    finally:
+        r.configure(None)
+
+
+@pytest.mark.parametrize('pose,w,h,nparts', [('P_id', 1920, 1080, 1), ('P_strafe', 1280, 720, 1), ('P_id', 1280, 720, 4)])
+def test_soup_matches_oracle(gpu_renderer, icosa_dir, pose, w, h, nparts):
+    """A triangle soup (the 2 000 icosahedra with no shared vertex, triangles shuffled): clusters
+    pooled along the Morton order and set up in a permuted order; ties still go to the lower slot."""
+    import torch
+    from swift3drenderer_amd.multi import assemble
+    path = icosa_dir['soup']
+    script = poses.script(pose)
+    want = oracle_render_pose(path, script, w, h, extra_frames=1)
+    r = gpu_renderer
+    got = render_pose(r, path, script, w, h, extra_frames=1)
+    cs = r.cluster_stats()
+    assert cs['clusters'] > 0 and cs['permuted'], cs
+    assert np.array_equal(got, want), diff(got, want)
+    if nparts > 1:
+        inp = (0, 0, 0, 0) + tuple(script[-1][4:6])
+        parts = []
+        for part in range(nparts):
+            rows = r.lib.s3r_band_rows_local(h, 16, nparts, part)
+            buf = torch.empty((rows, w), dtype=torch.int32, device='cuda')
+            r.render_bands(inp, w, h, 16, nparts, part, buf.data_ptr(), 0)
+            torch.cuda.synchronize()
+            parts.append(buf.cpu().numpy().view(np.uint32))
+        got = assemble(parts, h, 16)
+        assert np.array_equal(got, want), diff(got, want)
+
+
+@pytest.mark.parametrize('scene_name,pose,w,h', [('full', 'P_clip', 640, 480), ('full', 'P_over', 1000, 333),
+                                                 ('regular', 'P_over', 1280, 720), ('full', 'P_floor', 640, 480)])
+def test_forced_clusters_packaged(tiles, scene_dir, monkeypatch, scene_name, pose, w, h):
+    """Clusters on the packaged scenes (S3R_CLUSTERS=1 builds them for any scene): meshes crossing
+    the near plane (P_clip) and the 1 800-triangle floor cut into pieces, on the tile path."""
+    monkeypatch.setenv('S3R_CLUSTERS', '1')
+    path = scene_dir[scene_name]
+    script = poses.script(pose)
+    want = oracle_render_pose(path, script, w, h, extra_frames=1)
+    got = render_pose(tiles, path, script, w, h, extra_frames=1)
+    assert tiles.cluster_stats()['clusters'] > 0
     assert np.array_equal(got, want), diff(got, want)
 
 
@@ -155,8 +241,10 @@ def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
                                   ('stress', 'P_strafe', 1280, 720)])
 def test_vertex_stage_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeypatch, case):
     """The tile path with the vertex stage (S3R_VERTEX_STAGE=1: every vertex projected once by
-    k_tile_vertex, triangles set up from those; the near-plane clip recomputes its corners)."""
+    k_tile_vertex, triangles set up from those; the near-plane clip recomputes its corners) -- the
+    setup without clusters (S3R_CLUSTERS=0), where the vertex stage applies."""
     monkeypatch.setenv('S3R_VERTEX_STAGE', '1')
+    monkeypatch.setenv('S3R_CLUSTERS', '0')
     name, pose, w, h = case
     path = icosa_dir[2000] if name == 'stress' else scene_dir[name]
     gpu_renderer.set_raster_path('tiles')
