@@ -94,6 +94,32 @@ def cpu_baseline(data_path, script, hold, w, h, budget_s):
     return frames / el, frames, el
 
 
+def textured_scene(path, nv, ni, na, ntex) -> bool:
+    """Whether any attribute of the data.bin is textured (its disc tag, App. A, at +32 of the 48-B
+    record): only then can a frame sample texels.  Memory-mapped; a scene without textures is not
+    scanned."""
+    if not ntex or not na:
+        return False
+    import numpy as np
+    off = 16 + 16 * nv + 16 + 8 * (ni + ni % 2) + 16
+    rec = np.memmap(path, dtype=np.uint8, mode='r', offset=off, shape=(na, 48))
+    return bool(rec[:, 32:36].any())
+
+
+def frame_roofline(W, H, nv, ni, na, ntex, textured, device_s, delivered_s):
+    """SURVEY.md §8(d)'s whole-frame bytes B = 4 W H (framebuffer) + 16 V + 16 I + 48 A (the scene;
+    both index arrays at 8 B) + the texels when a textured triangle exists, against the device
+    frame time and the delivered (updateAndRender) median."""
+    b = 4 * W * H + 16 * nv + 16 * ni + 48 * na + (4 * ntex if textured else 0)
+    out = {'bytes_per_frame': b, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+           'formula': '4WH + 16V + 16I + 48A (+ 4 x texels if textured), SURVEY.md 8(d)'}
+    for k, t in (('device', device_s), ('delivered', delivered_s)):
+        if t:
+            out[f'achieved_{k}'] = round(b / t / 1e9, 2)
+            out[f'frac_{k}'] = round(b / t / 1e9 / HBM_PEAK_GBS, 5)
+    return out
+
+
 def load_traffic(workload_key):
     """HBM bytes per fragment launch from the committed rocprofv3 --pmc summary (profiles/)."""
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
@@ -202,6 +228,8 @@ def run_rank0(a, N, np, torch):
         call(hold_in)
 
     # value: synchronous updateAndRender calls, each timed like main.swift:120-122
+    r.device_profile()                     # (reset the per-device and fill profiles: timed calls only)
+    r.fill_profile()
     per = np.empty(steps)
     refs = [ctypes.byref(h) for h in buf.halves]
     in_ref = ctypes.byref(hold_in)
@@ -221,6 +249,8 @@ def run_rank0(a, N, np, torch):
 
     # both halves carry the held pose's frame; the pin state the frames were delivered with
     host = r.host_stats()
+    per_device = r.device_profile()        # each device's part: finish time after the call's entry, link bytes
+    fill_prof = r.fill_profile()           # host fill: devices' / fill threads' finish per frame (fill frames)
     halves_pinned = [bool(lib.s3r_host_pinned(ctypes.c_void_p(buf.ptr + k * buf.size), buf.size)) for k in (0, 1)]
     used = [m for m in ('copy', 'direct', 'fill') if host[f'{m}_frames'] > 0]
     link_bytes = host['link_bytes']
@@ -296,6 +326,8 @@ def run_rank0(a, N, np, torch):
         roof_rows, roof_launch = H, 'whole frame into HBM, frames pipelined (device_fps pass)'
         del out
     kernel, frag_bytes = kernel_bytes(roof_rows)
+    frame_roof = frame_roofline(W, H, nv, ni, na, ntex, textured_scene(data_path, nv, ni, na, ntex),
+                                1.0 / device_fps if device_fps else None, median_s)
     frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
     achieved = frag_bytes / frag_avg_s / 1e9
     workload = f'{a.scene}/{a.pose}/{W}x{H}/N1'
@@ -317,6 +349,10 @@ def run_rank0(a, N, np, torch):
         'n_gpus': N,
         'steps': steps,
         'warmup': warmup,
+        'steps_requested': a.steps,
+        'warmup_requested': a.warmup,
+        'steps_note': f'at least {MIN_TIMED} timed / {MIN_WARMUP} warm-up calls whatever --steps / --warmup say '
+                      '(SURVEY.md 8(d): fps = 1 / median of >= 200 calls)',
         'ms_per_step': round(total / steps * 1e3, 5),
         'higher_is_better': True,
         'scaling': 'strong',
@@ -337,7 +373,8 @@ def run_rank0(a, N, np, torch):
         'fps_mean': round(steps / total, 3),
         'frame_GB_per_s': round(frame_bytes / median_s / 1e9, 3),
         'delivery': {'mode': used[0] if len(used) == 1 else used, 'fill_threads': host['fill_threads'],
-                     'fill_gpu_eighths': host['fill_gpu_eighths'], 'link_bytes_per_frame': link_bytes, 'modes': modes},
+                     'fill_gpu_eighths': host['fill_gpu_eighths'], 'link_bytes_per_frame': link_bytes, 'modes': modes,
+                     'per_device': per_device, 'fill_profile': fill_prof},
         'link_roofline': {'bound': 'pcie', 'achieved': round(link_bytes / median_s / 1e9, 2),
                           'peak': LINK_PEAK_GBS * len(devices), 'unit': 'GB/s',
                           'frac': round(link_bytes / median_s / 1e9 / (LINK_PEAK_GBS * len(devices)), 5),
@@ -349,10 +386,12 @@ def run_rank0(a, N, np, torch):
         'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
         'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
         'fragment_kernel_ms_delivered': round(dl_frag_ms / max(dl_nfr, 1), 5),
+        # tile path: the per-triangle stages (cluster cull, setup, scan, fill) = device frame - fragment stage
+        'setup_fill_ms': round((frame_ms - frag_ms) / max(nfr, 1), 5) if path == 2 else None,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
                      'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,
-                     'launch': roof_launch},
+                     'launch': roof_launch, 'frame': frame_roof},
         'cpu_baseline': cpu,
     }
 

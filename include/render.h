@@ -170,8 +170,16 @@ void s3r_scene_counts(uint64_t out[8]);
  * frame whose counters were read back. */
 void s3r_tile_stats(uint64_t out[4]);
 
+/* Per device behind updateAndRender (s3r_configure_devices), for the frames since the last call:
+ * out[4 i] the device id, out[4 i + 1] the frames, out[4 i + 2] the sum of the times (ns after the
+ * call's entry) at which its part of each frame was in the caller's buffer, out[4 i + 3] the bytes
+ * it sent over its host link in the last frame.  Returns the device count (at most max_devices)
+ * and resets the sums.  Extension (a multi-GPU run's explanation; no render.cpp counterpart). */
+uint32_t s3r_device_profile(uint64_t *out, uint32_t max_devices);
+
 /* Tile path clusters (built at load for scenes the tile path renders, clusters.cpp): out[0] the
- * cluster count (0: none), out[1] 1 when the tile path culls them (S3R_CLUSTERS != 0), out[2] the
+ * cluster count (0: none), out[1] 1 when the tile path culls them (S3R_CLUSTERS: 0 never, 1 frame
+ * parts -- the default --, 2 whole frames too, and clusters for every scene), out[2] the
  * triangles of the clusters the last read-back frame kept, out[3] 1 when the setup order is a
  * permutation of the file order.  Extension: replaces nothing in render.cpp (render.cpp:297 visits
  * every triangle). */

@@ -1664,23 +1664,33 @@ __device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint
     d.rv = mk3(qx + half_w, qy + half_h, rz);                               // :288
 }
 
+// Exact a / b for small operands by one float multiply (the integer division by a run-time divisor
+// is ~20 instructions): inv = rcp(b) (1 + 2^-21) lies in [(1/b)(1 + 2^-22), (1/b)(1 + 2^-20)]
+// (v_rcp_f32 is within 1 ulp), so fl(a inv) is >= a / b and, when a / b = k + r / b with r >= 1,
+// below k + 1 as long as b (k + 1) < 2^19 -- true for a + b < 2^19 (rows, bands, tiles of frames
+// up to 65 535 px a side).  Truncation then gives k.
+__device__ __forceinline__ float udiv_inv(uint32_t b) { return __builtin_amdgcn_rcpf((float)b) * (1.0f + 0x1p-21f); }
+__device__ __forceinline__ uint32_t udiv_small(uint32_t a, float inv) { return (uint32_t)((float)a * inv); }
+
 // Local rows [lo, hi] of this rank that fall in frame rows [ymin, ymax] (interleaved bands: local
 // row order is frame row order, so the owned rows of any frame-row interval are one local range).
 __device__ __forceinline__ bool local_row_range(uint32_t ymin, uint32_t ymax, uint32_t band, uint32_t nparts,
                                                 uint32_t part, uint32_t &lo, uint32_t &hi) {
     if (nparts == 1u) { lo = ymin; hi = ymax; return ymin <= ymax; }
-    const uint32_t g0 = ymin / band, g1 = ymax / band;
+    const float ib = udiv_inv(band), ip = udiv_inv(nparts);
+    const uint32_t g0 = udiv_small(ymin, ib), g1 = udiv_small(ymax, ib);
+    const uint32_t m0 = g0 - udiv_small(g0, ip) * nparts, m1 = g1 - udiv_small(g1, ip) * nparts;
     uint32_t fg = g0, fy = ymin;
-    if (g0 % nparts != part) { fg = g0 + (part + nparts - g0 % nparts) % nparts; fy = fg * band; }
+    if (m0 != part) { fg = g0 + (part > m0 ? part - m0 : part + nparts - m0); fy = fg * band; }
     uint32_t lg = g1, ly = ymax;
-    if (g1 % nparts != part) {
-        const uint32_t d = (g1 % nparts + nparts - part) % nparts;
+    if (m1 != part) {
+        const uint32_t d = m1 > part ? m1 - part : m1 + nparts - part;
         if (g1 < d) return false;
         lg = g1 - d; ly = lg * band + band - 1u;
     }
     if (fg > lg || fy > ly) return false;
-    lo = (fg / nparts) * band + (fy - fg * band);
-    hi = (lg / nparts) * band + (ly - lg * band);
+    lo = udiv_small(fg, ip) * band + (fy - fg * band);
+    hi = udiv_small(lg, ip) * band + (ly - lg * band);
     return true;
 }
 
@@ -1721,7 +1731,9 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
         for (uint32_t q = 0; q < kSteps; q++) {
             const uint32_t k = k0 + q;
             const bool act = k < sp.n;
-            key[q] = act ? ((sp.ty0 + k / sp.ntx) * tiles_x + sp.tx0 + k % sp.ntx) * kDepthBuckets + sp.bucket
+            uint32_t ky = udiv_small(k, udiv_inv(sp.ntx));
+            if (sp.n >= (1u << 18)) ky = k / sp.ntx;          // (beyond udiv_small's range: huge boxes)
+            key[q] = act ? ((sp.ty0 + ky) * tiles_x + sp.tx0 + k - ky * sp.ntx) * kDepthBuckets + sp.bucket
                          : 0xFFFFFFFFu;
             uint64_t todo = __ballot(act);
             uint32_t my_leader = 0, my_rank = 0, cnt = 0;
@@ -1754,35 +1766,38 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
 // A strict upper bound of every 1/z the triangle can produce at a pixel it covers, i.e. of
 // ooz = (r0*a0 + r1*a1) + r2*a2 (render.cpp:363) over walked values a_i >= 0 (:362).  The walked
 // a_i of pixel (x, y) come from <= nx + ny float adds (:374, :378) through values inside the bbox,
-// where the exact affine w*_i(kx, ky) = ws_i + ky*dy_i + kx*dx_i is bounded by its corners: with M
-// the largest |w*_i| at a corner and S the largest corner sum of w*_0 + w*_1 + w*_2, each add rounds
-// by <= 2^-24 (M + 1), so a0 + a1 + a2 <= S + 3 (nx + ny) 2^-24 (M + 1); the three products and two
-// sums add <= 2^-22 relative (r_i = 1/z_i > 0 past the near plane).  Evaluated in double with a
-// further 2^-20 margin and rounded up.  A pixel whose current winner has a larger 1/z cannot be won
-// by this triangle (strict '>' at :364), so k_tile_raster may skip it.
+// where the exact affine w*_i(kx, ky) = ws_i + ky*dy_i + kx*dx_i is bounded by its corners: with
+// A_i = |ws_i| + ny |dy_i| + nx |dx_i| >= every |w*_i| and S the largest corner sum of w*_0 + w*_1 +
+// w*_2, each add rounds by <= 2^-24 (A + 1), so a0 + a1 + a2 <= S + 3 (nx + ny + 1) 2^-24 (A + 1);
+// the three products and two sums add <= 2^-22 relative (r_i = 1/z_i > 0 past the near plane).
+// Evaluated in float: the corner sums' own rounding is below 2^-21 sum A_i (covered by 2^-20 sum
+// A_i), the sum's by 2^-20 (|S| + slack), the product's by the final 2^-18.  A pixel whose current
+// winner has a larger 1/z cannot be won by this triangle (strict '>' at :364), so k_tile_raster may
+// skip it.
 __device__ float ooz_bound(const TriSetup &t) {
-    const double nx = (double)(t.xmax - t.xmin), ny = (double)(t.ymax - t.ymin);
-    double S = -1e300, M = 0.0;
+    const float nx = (float)(t.xmax - t.xmin), ny = (float)(t.ymax - t.ymin);   // (exact: < 2^16)
+    float S = -__builtin_inff(), sumA = 0.0f, Amax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float A = (fabsf(t.ws[i]) + ny * fabsf(t.dy[i])) + nx * fabsf(t.dx[i]);
+        sumA += A;
+        Amax = fmaxf(Amax, A);
+    }
 #pragma unroll
     for (int cx = 0; cx < 2; cx++) {
 #pragma unroll
         for (int cy = 0; cy < 2; cy++) {
-            double sum = 0.0;
+            float sum = 0.0f;
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const double w = (double)t.ws[i] + (cy ? ny : 0.0) * (double)t.dy[i] + (cx ? nx : 0.0) * (double)t.dx[i];
-                sum += w;
-                M = fmax(M, fabs(w));
-            }
-            S = fmax(S, sum);
+            for (int i = 0; i < 3; i++) sum += (t.ws[i] + (cy ? ny * t.dy[i] : 0.0f)) + (cx ? nx * t.dx[i] : 0.0f);
+            S = fmaxf(S, sum);
         }
     }
-    const double asum = S + 3.0 * (nx + ny + 1.0) * (M + 1.0) * 0x1p-24;
-    const double rmax = fmax(fmax((double)t.rvz[0], (double)t.rvz[1]), (double)t.rvz[2]);
-    const double b = rmax * asum * (1.0 + 0x1p-20) + 0x1p-126;
-    const float f = (float)b;
-    const float up = (double)f >= b ? f : u2f(f2u(f) + 1u);   // round up (b > 0)
-    return is_finite(up) && rmax > 0.0 && asum > 0.0 ? up : __builtin_inff();
+    const float slack = 3.0f * (nx + ny + 1.0f) * (Amax + 1.0f) * 0x1p-24f + 0x1p-20f * sumA;
+    const float asum = (S + slack) + 0x1p-20f * (fabsf(S) + slack);
+    const float rmax = fmaxf(fmaxf(t.rvz[0], t.rvz[1]), t.rvz[2]);
+    const float b = rmax * asum * (1.0f + 0x1p-18f) + 0x1p-126f;
+    return is_finite(b) && rmax > 0.0f && asum > 0.0f ? b : __builtin_inff();
 }
 
 __device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot, uint32_t zb) {
@@ -1849,9 +1864,11 @@ __device__ __forceinline__ bool cluster_meets(float4 s, const Mat34 &m, float fa
     const float z0 = nz - r, z1 = nz + r;
     if (!(z0 > 2.0f * kNear)) return true;                      // reaches the near plane: no bound
     // screen x = cv.x f / nz + W/2, y = -cv.y f / nz + H/2 (render.cpp:288) over the sphere
+    // (reciprocals within 1 ulp: far inside the pixel-plus-1e-5 margin below)
     const float ax = c.x - r, bx = c.x + r, ay = -c.y - r, by = -c.y + r;
-    const float xlo = (ax < 0 ? ax / z0 : ax / z1) * factor + sw / 2, xhi = (bx > 0 ? bx / z0 : bx / z1) * factor + sw / 2;
-    const float ylo = (ay < 0 ? ay / z0 : ay / z1) * factor + sh / 2, yhi = (by > 0 ? by / z0 : by / z1) * factor + sh / 2;
+    const float i0 = __builtin_amdgcn_rcpf(z0), i1 = __builtin_amdgcn_rcpf(z1);
+    const float xlo = (ax < 0 ? ax * i0 : ax * i1) * factor + sw / 2, xhi = (bx > 0 ? bx * i0 : bx * i1) * factor + sw / 2;
+    const float ylo = (ay < 0 ? ay * i0 : ay * i1) * factor + sh / 2, yhi = (by > 0 ? by * i0 : by * i1) * factor + sh / 2;
     const float mx = 1.0f + 1e-5f * (fabsf(xlo) + fabsf(xhi)), my = 1.0f + 1e-5f * (fabsf(ylo) + fabsf(yhi));
     if (xhi + mx < 0 || yhi + my < 0 || xlo - mx >= sw || ylo - my >= sh) return false;   // off screen
     if (nparts == 1u) return true;
@@ -1861,16 +1878,23 @@ __device__ __forceinline__ bool cluster_meets(float4 s, const Mat34 &m, float fa
 }
 
 // One thread per cluster (workgroup b: clusters 256 b ..., shard b % kTileShards): the surviving
-// clusters' triangle positions, appended to their shard's part of cmap.
+// clusters' triangle positions, appended to their shard's part of cmap (coalesced).  (Writing
+// {vertex indices, slot} records here instead, to spare the setup a dependent load, measured
+// worse: cull 21 -> 45 us, setup 133 -> 117 us at part 0 of 8.)
 __global__ void __launch_bounds__(256) k_cluster_cull(const float4 *__restrict__ sphere, const uint32_t *__restrict__ first,
-                                                      uint32_t ncl, const uint32_t *__restrict__ shard_tab, Mat34 m,
-                                                      float factor, float sw, float sh, uint32_t band, uint32_t nparts,
-                                                      uint32_t part, uint32_t *__restrict__ cmap, uint32_t *__restrict__ ctr) {
+                                                      uint32_t ncl, const uint32_t *__restrict__ shard_tab,
+                                                      Mat34 m, float factor, float sw, float sh, uint32_t band,
+                                                      uint32_t nparts, uint32_t part, uint32_t *__restrict__ cmap,
+                                                      uint32_t *__restrict__ ctr) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards;
     uint32_t n = 0, f0 = 0;
-    if (i < ncl && cluster_meets(sphere[i], m, factor, sw, sh, band, nparts, part)) {
-        f0 = first[i];
-        n = first[i + 1] - f0;
+    if (i < ncl) {
+        const float4 sp = sphere[i];
+        const uint32_t a = first[i], e = first[i + 1];
+        if (cluster_meets(sp, m, factor, sw, sh, band, nparts, part)) {
+            f0 = a;
+            n = e - a;
+        }
     }
     uint32_t inc = n;                                           // wave prefix sum of the sizes
     for (uint32_t o = 1; o < 64u; o <<= 1) {
@@ -1933,23 +1957,19 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
     tile_visit(sp, tiles_x, counts, nullptr, 0);
 }
 
-// The slot of position p (cluster order -> file order).
-template <bool CL>
-__device__ __forceinline__ uint32_t slot_of(uint32_t p, const uint32_t *__restrict__ cmap, const uint32_t *__restrict__ cperm) {
-    if (!CL) return p;
-    const uint32_t q = cmap[p];
-    return cperm ? cperm[q] : q;
-}
 
 // Setup, one lane per triangle; workgroup b serves shard s = b % kTileShards, grid-stride over the
-// shard's positions p = base(s) + j (with clusters: the cull's kept positions, slot_of).  A triangle
+// shard's positions p = base(s) + j (with clusters: the cull's kept positions cmap[p], each one's slot
+// cperm[cmap[p]] -- the identity when cperm is null -- loaded one iteration ahead; without: slot p).
+// A triangle
 // wholly past the near plane is set up here (emit_slot); one that crosses it (render.cpp:308, rare)
 // is queued for k_tile_clip -- the clip keeps it out of this loop's registers (occupancy: the
 // setup is memory-latency-bound).
 template <bool VS, bool CL>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, const uint32_t *__restrict__ cmap,
-                                                    const uint32_t *__restrict__ cperm, const uint32_t *__restrict__ shard_tab,
+                                                    const uint32_t *__restrict__ cperm,
+                                                    const uint32_t *__restrict__ shard_tab,
                                                     Mat34 m, float factor, float sw, float sh,
                                                     uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                     RasterRec *__restrict__ recs, uint4 *__restrict__ live,
@@ -1963,24 +1983,43 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     uint4 *const lv = live + 2ull * b0;
     uint32_t *const nlive = shard_ctr(ctr, 1, sh_id), *const nclip = shard_ctr(ctr, 2, sh_id);
     const float half_w = sw / 2, half_h = sh / 2;
-    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += per * 256u) {   // wave-uniform
+    // software pipeline over the loop's iterations: this iteration's slot and vertex indices were
+    // loaded during the previous one, the next iteration's are loaded during this one, and (with
+    // clusters) the cull's position for the one after that -- so an iteration waits for its corners
+    // only, not for the cmap -> slot -> index chain in front of them
+    const uint32_t step = per * 256u, jl = rank * 256u + threadIdx.x;
+    auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : b0 + jj; };
+    uint32_t t_cur = 0, vi_cur[3] = {0, 0, 0}, q_next = 0;
+    if (jl < n) {
+        t_cur = slot_at(jl, CL ? cmap[b0 + jl] : 0u);
+#pragma unroll
+        for (int k = 0; k < 3; k++) vi_cur[k] = vidx[3 * t_cur + k];
+    }
+    if (CL && jl + step < n) q_next = cmap[b0 + jl + step];
+    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += step) {   // wave-uniform
         const uint32_t j = j0 + lane;
         Vert d[3];
         TriSetup ts;
         bool live_t = false, clip = false;
-        uint32_t t = 0;
+        const uint32_t t = t_cur;
         if (j < n) {
-            t = slot_of<CL>(b0 + j, cmap, cperm);
 #pragma unroll
             for (int k = 0; k < 3; k++) {
-                const uint32_t vi = vidx[3 * t + k];
                 if (VS) {
-                    const float4 r = vrv[vi];                                      // the vertex stage's rv
+                    const float4 r = vrv[vi_cur[k]];                               // the vertex stage's rv
                     d[k].rv = mk3(r.x, r.y, r.z);
                 } else {
-                    load_corner(vtx, vi, m, factor, half_w, half_h, d[k]);
+                    load_corner(vtx, vi_cur[k], m, factor, half_w, half_h, d[k]);
                 }
             }
+        }
+        if (j + step < n) {                                     // the next iteration's slot and indices
+            t_cur = slot_at(j + step, q_next);
+#pragma unroll
+            for (int k = 0; k < 3; k++) vi_cur[k] = vidx[3 * t_cur + k];
+        }
+        if (CL && j + 2u * step < n) q_next = cmap[b0 + j + 2u * step];
+        if (j < n) {
             if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
                 clip = fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear;             // :308, rare
                 if (!clip) live_t = raster_part(d, sw, sh, ts);
@@ -1997,7 +2036,8 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
 template <bool CL>
 __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                    uint32_t ntri, const uint32_t *__restrict__ cmap,
-                                                   const uint32_t *__restrict__ cperm, const uint32_t *__restrict__ shard_tab,
+                                                   const uint32_t *__restrict__ cperm,
+                                                   const uint32_t *__restrict__ shard_tab,
                                                    Mat34 m, float factor, float sw, float sh,
                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                    RasterRec *__restrict__ recs, uint4 *__restrict__ live,
@@ -2017,7 +2057,11 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
         bool live_t = false, live_a = false;
         uint32_t t = 0;
         if (j < n) {
-            t = slot_of<CL>(clipq[b0 + j], cmap, cperm);
+            t = clipq[b0 + j];
+            if (CL) {
+                t = cmap[t];
+                if (cperm) t = cperm[t];
+            }
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
@@ -2039,8 +2083,9 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
 // overflow): workgroup 0 also writes the summary -- ctr[0] the live entries (summed over the
 // shards), ctr[1] the list length, ctr[2] the positions the cluster cull kept -- and, when sum_host
 // (host-coherent, 4 words) is given, the same three words then the frame's tag into it (system
-// scope, tag last: the host spins on it instead of a stream synchronisation); and every count is
-// reset to 0 for the set's next frame (k_tile_raster reads the offsets only; counts start zeroed).
+// scope, tag last: the host spins on it instead of a stream synchronisation); and every count, and
+// the shards' cull and clip counters, is reset to 0 for the set's next frame (k_tile_raster reads
+// the offsets only and resets the live counters once the fill has read them; all start zeroed).
 __global__ void __launch_bounds__(256) k_tile_cursor(uint32_t *__restrict__ counts, const uint32_t *__restrict__ offs,
                                                      uint32_t n, uint32_t *__restrict__ cursor, uint32_t *__restrict__ ctr,
                                                      uint32_t first, uint32_t *__restrict__ sum_host, uint32_t tag) {
@@ -2048,6 +2093,8 @@ __global__ void __launch_bounds__(256) k_tile_cursor(uint32_t *__restrict__ coun
     if (first && blockIdx.x == 0 && threadIdx.x < 64u) {
         static_assert(kTileShards == 64, "one lane per shard");
         uint32_t kept = *shard_ctr(ctr, 0, threadIdx.x), lv = *shard_ctr(ctr, 1, threadIdx.x);
+        *shard_ctr(ctr, 0, threadIdx.x) = 0u;                 // (read by the cull / setup / clip only)
+        *shard_ctr(ctr, 2, threadIdx.x) = 0u;
         for (int o = 32; o > 0; o >>= 1) {
             kept += (uint32_t)__shfl_xor((int)kept, o);
             lv += (uint32_t)__shfl_xor((int)lv, o);
@@ -2135,15 +2182,23 @@ __device__ __forceinline__ void slot_setup(uint32_t s, uint32_t ntri, const floa
 
 __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
-    uint32_t tiles_x, const uint32_t *__restrict__ offs, const uint32_t *__restrict__ counts,
-    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, const uint32_t *__restrict__ total,
-    uint32_t cap, uint32_t tile0) {
+    uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
+    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0) {
     __shared__ TileShared ls;
+    const uint32_t *const total = ctr + 1;
+    // the fill (complete before this launch) was the live counters' last reader: reset them for the
+    // set's next frame -- unless the list overflowed (the frame's fill runs again, render_api.cpp)
+    if (tile0 == 0u && blockIdx.x == 0u && threadIdx.x < kTileShards && *total <= cap)
+        *shard_ctr(ctr, 1, threadIdx.x) = 0u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = tile0 + blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t lx0 = tx * kTileW, lx1 = min(W, lx0 + kTileW) - 1u;
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
-    auto row_of = [&](uint32_t lr) { return nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band; };
+    const float ib = udiv_inv(band);
+    auto row_of = [&](uint32_t lr) {
+        const uint32_t g = udiv_small(lr, ib);
+        return nparts == 1u ? lr : (g * nparts + part) * band + (lr - g * band);
+    };
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
     // the tile's list: its depth buckets, nearest first, one after another
     const uint32_t s0 = tile * kDepthBuckets;
@@ -2706,10 +2761,12 @@ std::vector<uint32_t> cluster_shard_table(const std::vector<uint32_t> &first) {
 // once, so every workgroup runs from the start and the shards' loops end together -- a grid larger
 // than that leaves its late workgroups to run all their iterations after the others have finished),
 // fewer when there is less work.
-uint32_t shard_grid(const void *kernel, uint64_t work) {
-    // workgroups per shard: S3R_TILE_GRID = k (k > 0) or 0 (what the device keeps resident); default 128
-    static const int knob = getenv("S3R_TILE_GRID") ? atoi(getenv("S3R_TILE_GRID")) : 128;
-    uint64_t cap = knob > 0 ? (uint64_t)knob : 0;
+// Workgroups per shard: S3R_TILE_GRID = k (k > 0) or 0 (what the device keeps resident); default
+// `dflt` (measured on the stress scene: 256 for the cluster-culled frame parts' setup, 1024 -- about
+// one workgroup per 256 slots, no loop -- for whole frames).
+uint32_t shard_grid(const void *kernel, uint64_t work, uint32_t dflt = 256) {
+    static const int knob = getenv("S3R_TILE_GRID") ? atoi(getenv("S3R_TILE_GRID")) : -1;
+    uint64_t cap = knob > 0 ? (uint64_t)knob : knob < 0 ? dflt : 0;
     if (!cap) {
         static std::mutex mu;                      // (device worker threads launch concurrently)
         static std::map<const void *, uint32_t> resident;   // workgroups of 256 the device keeps resident
@@ -2727,8 +2784,8 @@ uint32_t shard_grid(const void *kernel, uint64_t work) {
     const uint64_t per = std::min<uint64_t>(cap, std::max<uint64_t>(1, (work / kTileShards + 255) / 256));
     return (uint32_t)(per * kTileShards);
 }
-template <class K> uint32_t shard_grid(K *kernel, uint64_t work) {
-    return shard_grid(reinterpret_cast<const void *>(kernel), work);
+template <class K> uint32_t shard_grid(K *kernel, uint64_t work, uint32_t dflt = 256) {
+    return shard_grid(reinterpret_cast<const void *>(kernel), work, dflt);
 }
 
 template <bool VS, bool CL>
@@ -2736,9 +2793,9 @@ void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const 
                   float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, void *recs,
                   uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv, hipStream_t st) {
     const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
-    hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri)), dim3(256), 0, st, vtx, vidx,
-                       ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq,
-                       ctr, counts, vrv);
+    hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
+                       0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx,
+                       (RasterRec *)recs, live, clipq, ctr, counts, vrv);
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
     hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
                        factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq, ctr, counts);
@@ -2749,8 +2806,7 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
                        uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag) {
-    const uint64_t ns = tile_slots(W, rows_local);
-    (void)hipMemsetAsync(ctr, 0, kTileCtrWords * sizeof(uint32_t), st);      // (counts: zeroed by k_tile_cursor)
+    const uint64_t ns = tile_slots(W, rows_local);        // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
         hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv);
@@ -2794,14 +2850,13 @@ void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, 
 }
 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                        uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st,
-                        uint32_t ty0, uint32_t ty1) {
+                        uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
+                        unsigned long long *keys, uint64_t cap, hipStream_t st, uint32_t ty0, uint32_t ty1) {
     const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
     ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
     if (tx == 0 || ty0 >= ty1) return;
     hipLaunchKernelGGL(k_tile_raster, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
-                       band, nparts, part, rows_local, tx, offs, counts, list, keys, total,
+                       band, nparts, part, rows_local, tx, offs, ctr, list, keys,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx);
 }
 

@@ -135,7 +135,7 @@ struct Dev {
     // init-time clusters (clusters.cpp): spheres, position ranges, position -> slot (null: identity),
     // and the cull's per-frame position list (one: every tile-path setup runs on geo[0])
     float4 *cl_sphere = nullptr;
-    uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_map = nullptr, *cl_shard = nullptr;
+    uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_shard = nullptr, *cl_map = nullptr;
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
@@ -330,6 +330,7 @@ struct Lib {
     uint64_t nindices = 0;
     uint32_t ncl = 0;                          // clusters (clusters.cpp; 0: the scene has none)
     bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
+    bool clusters_whole = false;               // ... also for whole frames (S3R_CLUSTERS=2)
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
@@ -381,6 +382,10 @@ struct Lib {
     // fill-thread placement: frames in a row whose buffer sat on another node than the placement's
     int fill_node_streak = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
+    // s3r_device_profile: per device behind updateAndRender, frames, the sum of its part's finish
+    // times (ns after the call's entry: rendered and in the caller's buffer) and its link bytes of
+    // the last frame
+    struct DevProf { uint64_t frames = 0, end_ns = 0, link_bytes = 0; } dev_prof[kMaxDevices];
 };
 
 Lib g;
@@ -524,10 +529,11 @@ HostScene read_scene() {
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
     // clusters for the tile path's per-frame cull (scenes the tile path renders by default, or any
-    // scene with S3R_CLUSTERS=1): connected meshes of 8-32 triangles, larger ones cut, smaller pooled
+    // scene with S3R_CLUSTERS=2): connected meshes of 8-32 triangles, larger ones cut, smaller pooled
     const char *ce = getenv("S3R_CLUSTERS");
     g.clusters = !(ce && atoi(ce) == 0);
-    if (g.clusters && (2 * ntri > kRowPathMaxSlots || (ce && atoi(ce) != 0)))
+    g.clusters_whole = ce && atoi(ce) == 2;
+    if (g.clusters && (2 * ntri > kRowPathMaxSlots || (ce && atoi(ce) == 2)))
         s3r_host::build_clusters(reinterpret_cast<const float *>(s.vtx.data()), (uint32_t)nv, s.vidx.data(),
                                  (uint32_t)ntri, 8, 32, s.cl_first, s.cl_sphere, s.cl_perm);
     g.ncl = s.cl_first.empty() ? 0 : (uint32_t)s.cl_first.size() - 1;
@@ -834,9 +840,13 @@ bool use_tile_path() {
     return 2ull * g.ntri > kRowPathMaxSlots;
 }
 
-// The device's clusters as the tile kernels take them (ncl 0: no cull, S3R_CLUSTERS=0 or none built).
-TileClusters tile_clusters(const Dev &d) {
-    return TileClusters{d.cl_sphere, d.cl_first, d.cl_perm, d.cl_shard, g.clusters ? g.ncl : 0u, d.cl_map};
+// The device's clusters as the tile kernels take them for a frame of nparts parts (ncl 0: no cull).
+// S3R_CLUSTERS: 0 never, 1 (default) for frame parts only -- a whole frame in view keeps nearly every
+// cluster, and the cull's records cost more than they save there (stress scene, one MI355X: whole
+// frame 96 us of cull for a 40 us shorter setup) -- 2 always.
+TileClusters tile_clusters(const Dev &d, uint32_t nparts) {
+    const bool on = g.clusters && g.ncl && (nparts > 1 || g.clusters_whole);
+    return TileClusters{d.cl_sphere, d.cl_first, d.cl_perm, d.cl_shard, on ? g.ncl : 0u, d.cl_map};
 }
 
 // The tile path's fill and fragment stage of buffer set p (its setup done): scatter into the set's
@@ -847,7 +857,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                          uint32_t rows_local, uint32_t *out, hipStream_t geo, hipStream_t st, TimingSlot *ts,
                          bool frame_rows) {
     const float sw = (float)W, sh = (float)d.tile_H;
-    const TileClusters cl = tile_clusters(d);
+    const TileClusters cl = tile_clusters(d, nparts);
     launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p], d.tile_list[p],
                      d.tile_list_cap[p], geo);
     HIPCHECK(hipEventRecord(d.geo_done[p], geo));
@@ -862,8 +872,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     uint32_t slabs = frame_rows ? g.tile_slabs : 1u;
     slabs = std::max(1u, std::min({slabs, tyn, kMaxTileSlabs}));
     if (slabs == 1u) {
-        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p],
-                           d.tile_list[p], d.keys, d.tile_total[p], d.tile_list_cap[p], st);
+        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], d.tile_list[p],
+                           d.keys, d.tile_list_cap[p], st);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
                             sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
                             g.tile_line_grid);
@@ -876,8 +886,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
         }
         for (uint32_t k = 0; k < slabs; k++) {
             const uint32_t ty0 = (uint32_t)((uint64_t)tyn * k / slabs), ty1 = (uint32_t)((uint64_t)tyn * (k + 1) / slabs);
-            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_counts[p],
-                               d.tile_list[p], d.keys, d.tile_total[p], d.tile_list_cap[p], st, ty0, ty1);
+            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
+                               d.tile_list[p], d.keys, d.tile_list_cap[p], st, ty0, ty1);
             HIPCHECK(hipEventRecord(d.slab_done[k], st));
             HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
             launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
@@ -963,7 +973,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     // for frame parts, where the per-triangle setup is replicated on every device; S3R_VERTEX_STAGE
     // = 0 / 1 forces it
     const char *vs_env = getenv("S3R_VERTEX_STAGE");
-    if (vs_env ? atoi(vs_env) != 0 : nparts > 1 && !(g.clusters && g.ncl)) {
+    if (vs_env ? atoi(vs_env) != 0 : nparts > 1 && !tile_clusters(d, nparts).ncl) {
         if (!d.vrv) d.vrv = dalloc<float4>(g.nv);
     } else if (d.vrv) {
         HIPCHECK(hipDeviceSynchronize());
@@ -976,19 +986,21 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
             d.live[p] = dalloc<uint4>((size_t)2 * g.ntri);
             if (!d.clipq) d.clipq = dalloc<uint32_t>(g.ntri);
             d.tile_ctr[p] = dalloc<uint32_t>(kTileCtrWords);
+            HIPCHECK(hipMemset(d.tile_ctr[p], 0, kTileCtrWords * sizeof(uint32_t)));
             d.tile_total[p] = d.tile_ctr[p] + 1;
         }
         HIPCHECK(hipHostMalloc((void **)&d.tile_sum_host, 4 * kSets * sizeof(uint32_t),
                                hipHostMallocCoherent | hipHostMallocMapped));
         memset(d.tile_sum_host, 0, 4 * kSets * sizeof(uint32_t));
         HIPCHECK(hipHostGetDevicePointer((void **)&d.tile_sum_dev, d.tile_sum_host, 0));
+        HIPCHECK(hipDeviceSynchronize());          // (the null-stream memsets vs the geometry streams)
     }
     const uint32_t p = next_set(d);
     hipStream_t geo = d.geo[0];
     HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[p], 0));
     if (g.serial) wait_all_fragments(d, geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
-    const TileClusters cl = tile_clusters(d);
+    const TileClusters cl = tile_clusters(d, nparts);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + 4 * p, d.frame_no);
@@ -1289,6 +1301,15 @@ void copy_bands_to_host(const uint32_t *dev_rows, uint32_t W, uint32_t H, uint32
 }
 
 // ---------------------------------------------------------------- updateAndRender's frame delivery
+// Device i's part of the frame is in the caller's buffer: its finish time and link bytes (profile).
+void note_device_done(int i, uint64_t link_bytes) {
+    Lib::DevProf &p = g.dev_prof[i];
+    p.frames++;
+    p.end_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                 g.call_t0).count();
+    p.link_bytes = link_bytes;
+}
+
 struct Delivery {
     uint32_t W, H, band, nparts;
     uint32_t *host;            // the caller's buffer (whole frame)
@@ -1331,6 +1352,7 @@ void deliver_part(void *arg, int i) {
         }
         HIPCHECK(hipStreamSynchronize(d.stream));
     }
+    note_device_done(i, job.nparts == 1 ? job.copy_bytes : (uint64_t)rows * job.W * 4);
 }
 
 // ---------------------------------------------------------------- deliveries
@@ -1569,7 +1591,9 @@ struct FillJob {
     // and the sky bins of the frame (the host's and the GPUs')
     std::atomic<int64_t> flags_ns{INT64_MAX}, sky_end_ns{0};
     std::atomic<uint64_t> sky_bins{0};
+    std::atomic<uint64_t> part_px[kMaxDevices] = {}, part_packed[kMaxDevices] = {};   // per part, as sky_px / packed_px
     int64_t issued_ns = 0;                                 // part 0's launches issued
+    std::chrono::steady_clock::time_point dev_done_ns[kMaxDevices];   // each device part's end
     int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
     uint64_t thread_px[65] = {};
     int64_t thread_widen_ns[65] = {};  // time in covered bins (widening, their background chunks)
@@ -1652,6 +1676,9 @@ void fill_worker(void *arg, int idx) {
     };
     uint32_t idle = 0;
     uint64_t px = 0, sky_bins = 0, packed = 0;
+    thread_local std::vector<uint64_t> ppx, ppk;            // per part: background / widened pixels
+    ppx.assign((size_t)job.nparts, 0);
+    ppk.assign((size_t)job.nparts, 0);
     int64_t widen_ns = 0;
     int64_t first_flag = -1, sky_end = 0;
     while (n) {
@@ -1683,6 +1710,7 @@ void fill_worker(void *arg, int idx) {
             if (part == 0 && b == 0 && (sky || (mask & 1u) || (job.stage && fp.rows_local && job.W >= fp.chunk_px)) &&
                 __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
+            const uint64_t px0 = px, pk0 = packed;
             if (!sky && job.stage) {
                 const auto w0 = std::chrono::steady_clock::now();
                 px += fill_bin(job, fp, b, sky, mask, &packed);
@@ -1690,6 +1718,8 @@ void fill_worker(void *arg, int idx) {
             } else {
                 px += fill_bin(job, fp, b, sky, mask, &packed);
             }
+            ppx[part] += px - px0;
+            ppk[part] += packed - pk0;
             if (sky) sky_end = since_start();
         }
         if (keep == n) {
@@ -1707,6 +1737,10 @@ void fill_worker(void *arg, int idx) {
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
     job.packed_px.fetch_add(packed, std::memory_order_relaxed);
+    for (int p = 0; p < job.nparts; p++) {
+        if (ppx[p]) job.part_px[p].fetch_add(ppx[p], std::memory_order_relaxed);
+        if (ppk[p]) job.part_packed[p].fetch_add(ppk[p], std::memory_order_relaxed);
+    }
     job.sky_bins.fetch_add(sky_bins, std::memory_order_relaxed);
     if (first_flag >= 0) {
         int64_t cur = job.flags_ns.load(std::memory_order_relaxed);
@@ -1763,6 +1797,7 @@ void deliver_part_direct(void *arg, int i) {
     // a tile-path frame whose list overflowed is rendered again, into the same rows
     if (fp.rows_local && job.W) tile_redo_if_overflowed(d, d.stream);
     note_end(job, job.dev_end_ns);
+    job.dev_done_ns[i] = std::chrono::steady_clock::now();
 }
 
 // One updateAndRender frame by direct delivery or host fill (fill).  kStaleMap: the caller's
@@ -1927,6 +1962,13 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
     const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
     (fill ? g.fill_frames : g.direct_frames)++;
     g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load() - job.packed_px.load()) + 3 * job.packed_px.load();
+    for (uint32_t i = 0; i < nparts; i++) {
+        Lib::DevProf &dp = g.dev_prof[i];
+        const uint64_t px = (uint64_t)job.parts[i].rows_local * W, sky = job.part_px[i].load(), pk = job.part_packed[i].load();
+        dp.frames++;
+        dp.end_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(job.dev_done_ns[i] - g.call_t0).count();
+        dp.link_bytes = 4 * (px - sky - pk) + 3 * pk;
+    }
     return stale ? kStaleMap : kMapped;
 }
 
@@ -2121,6 +2163,18 @@ __attribute__((visibility("default"))) void s3r_host_stats(uint64_t out[12]) {
     out[9] = (uint64_t)fill_threads(g.devs.size() > 1 ? (uint32_t)g.devs.size() : 1u);
     out[10] = g.link_bytes;
     out[11] = g.fill_gpu < 0 ? 0 : (uint64_t)g.fill_gpu;
+}
+
+__attribute__((visibility("default"))) uint32_t s3r_device_profile(uint64_t *out, uint32_t max_devices) {
+    const uint32_t n = std::min<uint32_t>((uint32_t)g.devs.size(), max_devices);
+    for (uint32_t i = 0; i < n; i++) {
+        out[4 * i] = (uint64_t)g.devs[i]->device;
+        out[4 * i + 1] = g.dev_prof[i].frames;
+        out[4 * i + 2] = g.dev_prof[i].end_ns;
+        out[4 * i + 3] = g.dev_prof[i].link_bytes;
+        g.dev_prof[i] = Lib::DevProf{};
+    }
+    return n;
 }
 
 __attribute__((visibility("default"))) uint32_t s3r_fill_profile(uint64_t *out, uint32_t max_threads) {

@@ -109,7 +109,8 @@ struct TileClusters {
 constexpr uint32_t kTileShards = 64, kTileShardStride = 64;
 // Shard s's first position: the triangles of the clusters of shards < s (kTileShards + 1 entries).
 std::vector<uint32_t> cluster_shard_table(const std::vector<uint32_t> &first);
-// ctr: kTileCtrWords device words per frame (zeroed by launch_tile_setup): [0] live entries, [1] the
+// ctr: kTileCtrWords device words per buffer set (allocate them zeroed; the tile kernels leave the
+// shard counters zero again after each frame): [0] live entries, [1] the
 // tile lists' total length, [2] positions the cluster cull kept (the first kTileCounterWords are
 // the summary the host reads back), then the shards' counters.  live: 2T entries (tile box, rows,
 // slot, 0); clipq: T words (the positions whose triangle crosses the near plane).  cl (may be null
@@ -137,9 +138,11 @@ void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, 
                       uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
                       hipStream_t st);
 // keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
+// ctr: the setup's counters (its list length ctr[1]; the launch of tile row 0 resets the live counters
+// when the list did not overflow).
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                        uint32_t rows_local, const uint32_t *offs, const uint32_t *counts, const uint32_t *list,
-                        unsigned long long *keys, const uint32_t *total, uint64_t cap, hipStream_t st,
+                        uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
+                        unsigned long long *keys, uint64_t cap, hipStream_t st,
                         uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu);   // tile rows [ty0, ty1) only
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,

@@ -77,6 +77,9 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_fill_profile.restype = ctypes.c_uint32
     lib.s3r_tile_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_tile_stats.restype = None
+    if hasattr(lib, 's3r_device_profile'):
+        lib.s3r_device_profile.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+        lib.s3r_device_profile.restype = ctypes.c_uint32
     if hasattr(lib, 's3r_cluster_stats'):         # (optional: A/B runs load earlier builds via S3R_LIB)
         lib.s3r_cluster_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
         lib.s3r_cluster_stats.restype = None
@@ -150,6 +153,16 @@ class Renderer:
         self.lib.s3r_tile_stats(out)
         return {'readbacks': int(out[0]), 'overflows': int(out[1]), 'last_pairs': int(out[2]),
                 'last_live': int(out[3])}
+
+    def device_profile(self) -> list:
+        """Per device behind updateAndRender since the last call (include/render.h
+        s3r_device_profile): mean finish time of its part (us after the call's entry) and its link
+        bytes in the last frame."""
+        out = (ctypes.c_uint64 * (4 * 64))()
+        n = self.lib.s3r_device_profile(out, 64)
+        return [{'device': int(out[4 * i]), 'frames': int(out[4 * i + 1]),
+                 'finish_us': round(out[4 * i + 2] / max(out[4 * i + 1], 1) / 1e3, 2),
+                 'link_bytes': int(out[4 * i + 3])} for i in range(n)]
 
     def cluster_stats(self) -> dict:
         """Tile path clusters (include/render.h s3r_cluster_stats)."""

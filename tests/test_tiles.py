@@ -78,17 +78,20 @@ def test_stress_small_matches_oracle(gpu_renderer, icosa_dir, pose, w, h):
     assert np.array_equal(got, want), diff(got, want)
 
 
-@pytest.mark.parametrize('clusters', ['1', '0'])
+@pytest.mark.parametrize('clusters', ['2', '1', '0'])
 def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir, oracle_100k_4k, monkeypatch, clusters):
     """100 000 icosahedra (2 M triangles) at 3840x2160 -- a tenth of config 5, oracle-checkable --
-    with the cluster cull (the default) and without (S3R_CLUSTERS=0)."""
+    with the cluster cull on whole frames (S3R_CLUSTERS=2), for frame parts only (the default) and
+    off (S3R_CLUSTERS=0)."""
     monkeypatch.setenv('S3R_CLUSTERS', clusters)
     path = icosa_dir[100000]
     want = oracle_100k_4k
     got = render_pose(gpu_renderer, path, poses.script('P_id'), 3840, 2160)
     assert (want != 0x1E1E1E).mean() > 0.9            # the view is filled
     assert np.array_equal(got, want), diff(got, want)
-    assert gpu_renderer.cluster_stats()['clusters'] == (100000 if clusters == '1' else 0)
+    cs = gpu_renderer.cluster_stats()
+    assert cs['clusters'] == (0 if clusters == '0' else 100000), cs
+    assert cs['culling'] == (clusters != '0'), cs
 
 
 @pytest.mark.parametrize('nparts', [8, 3])
@@ -125,9 +128,11 @@ def test_stress_100k_4k_parts_match_oracle(gpu_renderer, icosa_dir, oracle_100k_
 
 
 @pytest.mark.parametrize('pose,w,h,nparts', [('P_id', 1920, 1080, 1), ('P_strafe', 1280, 720, 1), ('P_id', 1280, 720, 4)])
-def test_soup_matches_oracle(gpu_renderer, icosa_dir, pose, w, h, nparts):
+def test_soup_matches_oracle(gpu_renderer, icosa_dir, monkeypatch, pose, w, h, nparts):
     """A triangle soup (the 2 000 icosahedra with no shared vertex, triangles shuffled): clusters
-    pooled along the Morton order and set up in a permuted order; ties still go to the lower slot."""
+    pooled along the Morton order and set up in a permuted order; ties still go to the lower slot.
+    Whole frames culled too (S3R_CLUSTERS=2)."""
+    monkeypatch.setenv('S3R_CLUSTERS', '2')
     import torch
     from swift3drenderer_amd.multi import assemble
     path = icosa_dir['soup']
@@ -154,9 +159,10 @@ def test_soup_matches_oracle(gpu_renderer, icosa_dir, pose, w, h, nparts):
 @pytest.mark.parametrize('scene_name,pose,w,h', [('full', 'P_clip', 640, 480), ('full', 'P_over', 1000, 333),
                                                  ('regular', 'P_over', 1280, 720), ('full', 'P_floor', 640, 480)])
 def test_forced_clusters_packaged(tiles, scene_dir, monkeypatch, scene_name, pose, w, h):
-    """Clusters on the packaged scenes (S3R_CLUSTERS=1 builds them for any scene): meshes crossing
-    the near plane (P_clip) and the 1 800-triangle floor cut into pieces, on the tile path."""
-    monkeypatch.setenv('S3R_CLUSTERS', '1')
+    """Clusters on the packaged scenes (S3R_CLUSTERS=2 builds them for any scene and culls whole
+    frames): meshes crossing the near plane (P_clip) and the 1 800-triangle floor cut into pieces,
+    on the tile path."""
+    monkeypatch.setenv('S3R_CLUSTERS', '2')
     path = scene_dir[scene_name]
     script = poses.script(pose)
     want = oracle_render_pose(path, script, w, h, extra_frames=1)

@@ -2,6 +2,8 @@
 # Hardware-counter passes over the bench workload (one rocprofv3 --pmc pass per counter group;
 # FETCH_SIZE and WRITE_SIZE each need their own pass on gfx950).  Usage (on the GPU box):
 #   bash tools/pmc.sh <outdir> [bench args...]
+# PMC_CMD overrides the profiled command (default: python3 bench.py <args>), e.g.
+#   PMC_CMD="python3 tools/overhead_probe.py --scene icosa-stress --nparts 8 --steps 10 --data /tmp/s.bin"
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
 ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline --no-e2e}
@@ -17,6 +19,6 @@ for grp in \
   "WRITE_SIZE" \
   "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$ROOTDIR/$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$ROOTDIR/$OUT/p$i" -o run -- ${PMC_CMD:-python3 bench.py $ARGS} > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
 python3 tools/pmc_summary.py "$OUT"

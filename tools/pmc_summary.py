@@ -22,7 +22,7 @@ def main():
     ap.add_argument('--workload', default=None)
     a = ap.parse_args()
     acc = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(a.dir, 'pmc*', '**', '*counter_collection.csv'), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(a.dir, '**', '*counter_collection.csv'), recursive=True)):
         rows = defaultdict(lambda: defaultdict(float))
         with open(f) as fh:
             for row in csv.DictReader(fh):

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 for spec in "$@"; do
   IFS='|' read -r tag lib envs <<< "$spec"
   for n in ${NS:-1 8}; do
-    env $envs ${lib:+S3R_LIB=$lib} timeout -k 10 300 python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data /tmp/s3r_stress.bin --nparts $n --steps ${STEPS:-30} 2>/dev/null \
+    env $envs ${lib:+S3R_LIB=$lib} timeout -k 10 300 python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data /tmp/s3r_stress.bin --nparts $n --band ${BAND:-16} --steps ${STEPS:-30} 2>/dev/null \
       | grep '^{' | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag N=$n', round(1e6/d['wall_us']), 'fps  frag', round(d['frag_us'],1), 'frame', round(d['frame_us'],1))" || exit 1
   done
 done
