@@ -104,6 +104,15 @@ int64_t s3r_render_bands(const Input *input, uint32_t width, uint32_t height, ui
 int64_t s3r_bands_to_host(const uint32_t *dev_rows, uint32_t width, uint32_t height, uint32_t band_rows,
                           uint32_t n_parts, uint32_t part, uint32_t *host_frame, void *stream);
 
+/* One process per GPU, frames kept in HBM: after one RCCL gather has put the N parts'
+ * compact band buffers on GPU 0 one after another (part p's rows from row p * part_stride_rows of
+ * `gathered`, device memory), write the W x H frame in row order into `frame` (device memory) on
+ * `stream`, asynchronously -- one kernel.  Returns 0, or -1 on bad arguments (a part with more rows
+ * than part_stride_rows).  Extension: the multi-GPU reassembly; render.cpp renders the whole frame
+ * (render.cpp:264-265). */
+int s3r_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_rows, uint32_t width, uint32_t height,
+                           uint32_t band_rows, uint32_t n_parts, uint32_t *frame, void *stream);
+
 /* Drop the library's page-lock of a caller host buffer starting at ptr (waits for the device first);
  * a no-op for a pointer the library never registered.  For host frames about to be unmapped or freed
  * (updateAndRender buffers need not: a stale registration is detected and replaced there). */

@@ -1303,11 +1303,13 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         carry = rot;
     };
     // HOSTW with pstage (packed delivery, render_api.cpp): a whole covered chunk goes over the link
-    // at 3 bytes a pixel into the staging frame (row y at stage + 3 W y) -- 192 bytes, lanes 0..47 one
-    // dword each, gathered from the lanes of its pixels -- and the host widens it into the caller's
-    // buffer once the bin's chunk mask is in; a chunk cut by the frame's right edge is stored
-    // directly.  The link carries 3/4 of the covered pixels' bytes.
-    uint8_t *const srow = (HOSTW && pstage) ? pstage + (size_t)3u * W * y : nullptr;
+    // at 3 bytes a pixel into the staging frame -- bin-major: bin b's rows x segment pixels at
+    // pstage + b x (kWaves x segment x 3), its row (wave) w at + w x segment x 3 -- 192 bytes, lanes
+    // 0..47 one dword each, gathered from the lanes of its pixels; the host widens it into the
+    // caller's buffer once the bin's chunk mask is in; a chunk cut by the frame's right edge is
+    // stored directly.  The link carries 3/4 of the covered pixels' bytes.
+    constexpr uint32_t kSegStage = 3u * kChunk * SEGCH;
+    uint8_t *const srow = (HOSTW && pstage) ? pstage + (size_t)bid * (kWaves * kSegStage) + wave * kSegStage : nullptr;
     auto put_packed = [&](uint32_t c0x, uint32_t v) {
         const uint32_t b = 4u * lane, i0 = b / 3u, o = b - 3u * i0;
         const uint32_t a0 = (uint32_t)__shfl((int)v, (int)min(i0, 63u));
@@ -1317,7 +1319,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         // system-scope stores: their completion (the s_waitcnt before the chunk mask) is their arrival
         // in host memory, so the host never reads a staged chunk before its bytes
         if (lane < 48u)
-            __hip_atomic_store(reinterpret_cast<uint32_t *>(srow + 3u * c0x) + lane, w, __ATOMIC_RELAXED,
+            __hip_atomic_store(reinterpret_cast<uint32_t *>(srow + 3u * (c0x - xs)) + lane, w, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     };
     S3R_WGC_DECL;
@@ -2733,6 +2735,41 @@ void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, u
     }
     hipExtLaunchKernelGGL(k_sky_flags, dim3(blocks), dim3(256), 0, st, nullptr, done, 0, bincnt, (uint32_t)nbins, flags,
                           tag, probe, gpu_eighths);
+}
+
+// ------------------------------------------------------------------ band de-interleave
+// The gathered parts (part p's compact rows at gathered + p * part_stride_rows * W, as one RCCL gather
+// leaves them on GPU 0) -> the W x H frame in row order (frame row y belongs to part
+// (y / band) % nparts, local row (y / band / nparts) * band + y % band).  One thread per 4 pixels
+// (16-B loads and stores when W % 4 == 0 and both buffers are 16-B aligned); grid (x blocks, H).
+template <bool V4>
+__global__ void __launch_bounds__(256) k_deinterleave_bands(const uint32_t *__restrict__ gathered, uint32_t part_stride_rows,
+                                                            uint32_t W, uint32_t band, uint32_t nparts,
+                                                            uint32_t *__restrict__ frame) {
+    const uint32_t y = blockIdx.y, g = y / band, part = g % nparts, lr = (g / nparts) * band + y % band;
+    const uint32_t *src = gathered + ((size_t)part * part_stride_rows + lr) * W;
+    uint32_t *dst = frame + (size_t)y * W;
+    const uint32_t x = (blockIdx.x * 256u + threadIdx.x) * 4u;
+    if (V4) {
+        if (x < W) *reinterpret_cast<uint4 *>(dst + x) = *reinterpret_cast<const uint4 *>(src + x);
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (x + k < W) dst[x + k] = src[x + k];
+    }
+}
+
+void launch_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_rows, uint32_t W, uint32_t H,
+                               uint32_t band, uint32_t nparts, uint32_t *frame, hipStream_t st) {
+    if (!W || !H) return;
+    const dim3 grid((W + 1023u) / 1024u, H);
+    const bool v4 = W % 4 == 0 && ((uintptr_t)gathered & 15u) == 0 && ((uintptr_t)frame & 15u) == 0;
+    if (v4)
+        hipLaunchKernelGGL(k_deinterleave_bands<true>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band, nparts,
+                           frame);
+    else
+        hipLaunchKernelGGL(k_deinterleave_bands<false>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band,
+                           nparts, frame);
 }
 
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }

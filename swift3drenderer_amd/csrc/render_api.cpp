@@ -1569,6 +1569,8 @@ int fill_threads(uint32_t nparts = 1) {
 }
 
 struct FillPart {
+    size_t stage_off;                // packed delivery: this part's bins in the staging frame (bytes)
+    uint32_t bin_bytes;              // ... one bin's staged pixels: rows x segment x 3 bytes, contiguous
     uint32_t *flags;                 // host view of the device's sky flags
     unsigned long long *chunks;      // host view of its covered bins' chunk masks
     uint32_t tag, seg_px, segs, rpb, chunk_px, rows_local, band, nparts, part;
@@ -1620,14 +1622,8 @@ uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, 
     if (!sky && job.stage) {
         // the bin's staged rows are cold (just written by the device): request all their lines at
         // once, so the widening below waits for memory once per bin, not once per chunk
-        for (uint32_t k = 0; k < fp.rpb; k++) {
-            const uint32_t lr = blk * fp.rpb + k;
-            if (lr >= fp.rows_local) break;
-            const uint32_t y = ((lr / fp.band) * fp.nparts + fp.part) * fp.band + lr % fp.band;
-            if (y >= job.H) continue;
-            const uint8_t *a = job.stage + 3 * ((size_t)y * job.W + xs), *e = job.stage + 3 * ((size_t)y * job.W + xe);
-            for (; a < e; a += 64) __builtin_prefetch(a, 0, 0);
-        }
+        const uint8_t *a = job.stage + fp.stage_off + b * fp.bin_bytes, *e = a + fp.bin_bytes;
+        for (; a < e; a += 64) __builtin_prefetch(a, 0, 0);
     }
     for (uint32_t k = 0; k < fp.rpb; k++) {
         const uint32_t lr = blk * fp.rpb + k;
@@ -1647,7 +1643,8 @@ uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, 
                 s3r_host::fill_words(row + c0, c1 - c0, kBackground);
                 px += c1 - c0;
             } else if (job.stage && c1 - c0 == fp.chunk_px) {
-                s3r_host::widen_pixels(job.stage + 3 * ((size_t)y * job.W + c0), row + c0, fp.chunk_px);
+                s3r_host::widen_pixels(job.stage + fp.stage_off + b * fp.bin_bytes + 3 * ((size_t)k * fp.seg_px + (c0 - xs)),
+                                       row + c0, fp.chunk_px);
                 *packed += fp.chunk_px;
             }
         }
@@ -1862,12 +1859,26 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             g.fill_placed = !cpus.empty();
         }
     }
+    const uint32_t band = nparts == 1 ? H : g.band;
+    for (uint32_t i = 0; i < nparts; i++) {                 // the parts' bin layouts
+        FillPart &fp = job.parts[i];
+        fp.rows_local = nparts == 1 ? H : band_rows_local(H, band, nparts, i);
+        const FragLayout l = fragment_layout(W, fp.rows_local);
+        fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.chunk_px = l.chunk_px;
+        fp.bins = fp.rows_local ? l.bins : 0;
+        fp.band = band; fp.nparts = nparts; fp.part = i;
+        fp.bin_bytes = fp.rpb * fp.seg_px * 3u;
+        fp.stage_off = i == 0 ? 0 : job.parts[i - 1].stage_off + job.parts[i - 1].bins * job.parts[i - 1].bin_bytes;
+    }
     // packed delivery (host fill only): the staging frame, 3 bytes a pixel, mapped on every device
     if (fill && pack_enabled()) {
         // ordinary (CPU-cacheable) pages, registered plainly for the devices: the fill threads read
         // it at memory speed (hipHostMalloc's pages, or an uncached registration, read ~10x slower);
         // its rows are 64-B aligned, so the GPUs' whole-line stores need no uncached mapping
-        const size_t bytes = ((size_t)3 * W * H + 64 + 4095) & ~(size_t)4095;
+        // bin-major: each bin's rows x segment pixels contiguous (the fill threads stream through their
+        // blocks of bins instead of gathering a bin's 1-KB row pieces, 3 W bytes apart)
+        const FillPart &lp = job.parts[nparts - 1];
+        const size_t bytes = (lp.stage_off + lp.bins * lp.bin_bytes + 64 + 4095) & ~(size_t)4095;
         if (g.stage_cap < bytes) {
             drain_devices();
             HIPCHECK(hipSetDevice(g.devs[0]->device));
@@ -1890,15 +1901,9 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             }
         }
     }
-    const uint32_t band = nparts == 1 ? H : g.band;
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
         FillPart &fp = job.parts[i];
-        fp.rows_local = nparts == 1 ? H : band_rows_local(H, band, nparts, i);
-        const FragLayout l = fragment_layout(W, fp.rows_local);
-        fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.chunk_px = l.chunk_px;
-        fp.bins = fp.rows_local ? l.bins : 0;
-        fp.band = band; fp.nparts = nparts; fp.part = i;
         if (!fill) {
             job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0, nullptr};
             continue;
@@ -1926,7 +1931,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
         fp.chunks = d.fill_chunks;
         fp.tag = d.fill_tag;
         job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu,
-                             job.stage ? d.stage_dev : nullptr};
+                             job.stage ? d.stage_dev + fp.stage_off : nullptr};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
@@ -2126,6 +2131,19 @@ __attribute__((visibility("default"))) int64_t s3r_bands_to_host(const uint32_t 
     host_pinned(host_frame, (size_t)width * height * sizeof(uint32_t));
     copy_bands_to_host(dev_rows, width, height, band_rows, n_parts, part, host_frame, (hipStream_t)stream);
     return rows;
+}
+
+__attribute__((visibility("default"))) int s3r_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_rows,
+                                                                 uint32_t width, uint32_t height, uint32_t band_rows,
+                                                                 uint32_t n_parts, uint32_t *frame, void *stream) {
+    if (band_rows == 0 || n_parts == 0 || ((!gathered || !frame) && width && height)) return -1;
+    for (uint32_t p = 0; p < n_parts; p++)            // every part's rows must fit its stride
+        if (band_rows_local(height, band_rows, n_parts, p) > part_stride_rows) return -1;
+    if (g.initialized) HIPCHECK(hipSetDevice(g.devs[0]->device));
+    else if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
+    launch_deinterleave_bands(gathered, part_stride_rows, width, height, band_rows, n_parts, frame, (hipStream_t)stream);
+    HIPCHECK(hipGetLastError());
+    return 0;
 }
 
 __attribute__((visibility("default"))) void s3r_unregister_host(void *ptr) {

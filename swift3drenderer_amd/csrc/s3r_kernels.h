@@ -19,9 +19,11 @@ namespace s3r {
 // bins that end without a winner:
 // each bin's workgroup stores chunk_flags[bin] = (fill_tag << 32) | mask at its end, bit
 // (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.  stage (with
-// frame_rows and host_fill; device address of a 3 W H byte host buffer): every other chunk that lies
-// wholly inside the frame is stored there packed at 3 bytes a pixel (frame row y at stage + 3 W y,
-// little-endian b, g, r) instead of into out, for the host to widen (complete before the mask).
+// frame_rows and host_fill; device address of a host buffer of bins x rows_per_bin x segment x 3
+// bytes): every other chunk that lies wholly inside the frame is stored there packed at 3 bytes a
+// pixel (bin-major: bin b at stage + b x rows_per_bin x segment x 3, its row r at + r x segment x
+// 3, the chunk at + 3 x (x - segment start); little-endian b, g, r) instead of into out, for the
+// host to widen (complete before the mask).
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
@@ -151,6 +153,11 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          uint32_t rows_local, hipStream_t st, bool frame_rows = false,
                          uint32_t r0 = 0, uint32_t r1 = 0xFFFFFFFFu,      // local rows [r0, r1) only (r0 % 4 == 0)
                          bool line_grid = false);   // frame_rows: wave stores on the caller's 64-B line grid
+
+// The N parts of an interleaved band split, gathered one after another (part p's compact rows from
+// row p * part_stride_rows), written into the W x H frame in frame-row order (one launch).
+void launch_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_rows, uint32_t W, uint32_t H,
+                               uint32_t band, uint32_t nparts, uint32_t *frame, hipStream_t st);
 
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);

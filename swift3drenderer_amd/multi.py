@@ -49,6 +49,22 @@ class BandGather:
         """Collective: every rank's `send` (rows [0, rows) valid) -> rank 0's `frame`."""
         dist.gather(self.send, self.recv, dst=0, group=group)
         if self.rank == 0:
+            self.deinterleave()
+        return self.frame
+
+    def deinterleave(self):
+        """Rank 0: the gathered parts in `recv_all` -> `frame` in row order.  On the GPU this is the
+        library's one-launch kernel (include/render.h s3r_deinterleave_bands) on the current stream;
+        the gloo path (CPU tensors, tests) uses a row gather."""
+        if self.recv_all.is_cuda:
+            from .renderer import load_library
+            lib = load_library()
+            st = torch.cuda.current_stream(self.recv_all.device).cuda_stream
+            rc = lib.s3r_deinterleave_bands(self.recv_all.data_ptr(), self.max_rows, self.W, self.H, self.B, self.N,
+                                            self.frame.data_ptr(), st)
+            if rc != 0:
+                raise RuntimeError('s3r_deinterleave_bands rejected the split')
+        else:
             torch.index_select(self.recv_all, 0, self.src_rows, out=self.frame)
         return self.frame
 

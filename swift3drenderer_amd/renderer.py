@@ -77,6 +77,10 @@ def load_library(path: str = LIB_PATH):
     lib.s3r_fill_profile.restype = ctypes.c_uint32
     lib.s3r_tile_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.s3r_tile_stats.restype = None
+    if hasattr(lib, 's3r_deinterleave_bands'):     # (optional: A/B runs load earlier builds via S3R_LIB)
+        lib.s3r_deinterleave_bands.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        lib.s3r_deinterleave_bands.restype = ctypes.c_int
     if hasattr(lib, 's3r_device_profile'):
         lib.s3r_device_profile.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
         lib.s3r_device_profile.restype = ctypes.c_uint32

@@ -228,3 +228,57 @@ def test_gpu_bands_to_host_after_unregister(gpu_renderer, scene_dir):
         assert np.array_equal(host, want), f'delivery {rep}'
     r.unregister_host(host)
     print(f'new frame at the old address {same} of 2 times')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('w,h,band,n', [(3840, 2160, 16, 8), (1000, 333, 7, 3), (1918, 1080, 16, 4)])
+def test_gpu_deinterleave_matches_oracle(gpu_renderer, scene_dir, w, h, band, n):
+    """The library's de-interleave kernel (s3r_deinterleave_bands, BandGather.deinterleave): N parts
+    rendered with s3r_render_bands into their slots of one gather buffer, exactly as one RCCL gather
+    leaves them on GPU 0, reassembled on the GPU == the oracle's frame (widths that are and are not
+    multiples of 4: the 16-B and the scalar kernel)."""
+    from oracle.oracle import render_pose
+    from swift3drenderer_amd import poses
+    script = poses.script('P_over')
+    want = render_pose(scene_dir['full'], script, w, h)
+    r = gpu_renderer
+    r.configure(scene_dir['full'])
+    for t in script:
+        r.update_and_render(w, h, t)
+    hold = poses.hold('P_over')
+    bg = BandGather(w, h, band, n, 0, torch.device('cuda'))
+    bg.recv_all.fill_(-1)
+    for p in range(n):
+        assert r.render_bands(hold, w, h, band, n, p, bg.recv[p].data_ptr(), 0) == band_rows(h, band, n, p)
+    torch.cuda.synchronize()
+    got = bg.deinterleave()
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want)
+    assert r.lib.s3r_deinterleave_bands(bg.recv_all.data_ptr(), bg.max_rows - 1, w, h, band, n,
+                                        bg.frame.data_ptr(), 0) == -1      # a stride too short is refused
+
+
+@pytest.mark.gpu
+def test_nccl_gather_one_rank(gpu_renderer, scene_dir):
+    """BandGather over torch.distributed's nccl backend (RCCL) in this process, world size 1: the RCCL
+    gather executes on the GPU and the frame comes out whole (this pool's boxes have one GPU; the
+    N-rank path is the same call)."""
+    from oracle.oracle import render_pose
+    from swift3drenderer_amd import poses
+    w, h = 640, 480
+    script = poses.script('P_over')
+    want = render_pose(scene_dir['full'], script, w, h)
+    r = gpu_renderer
+    r.configure(scene_dir['full'])
+    for t in script:
+        r.update_and_render(w, h, t)
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{free_port()}', rank=0, world_size=1)
+    try:
+        bg = BandGather(w, h, 16, 1, 0, torch.device('cuda'))
+        r.render_bands(poses.hold('P_over'), w, h, 16, 1, 0, bg.send.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+        got = bg.gather()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want)

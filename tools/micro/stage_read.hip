@@ -67,8 +67,9 @@ int main() {
     uint32_t *frame = (uint32_t *)aligned_alloc(4096, (npx * 4 + 64 + 4095) & ~(size_t)4095);
     memset(frame, 0, npx * 4);
     auto doms = domains();
-    const int T = 4;
+    int T = 4;
     size_t piece = 64;
+    bool blocks = false;          // false: pieces in a hashed order; true: blocks of 8 consecutive pieces per thread
     auto run_widen = [&](const char *what) {
         auto t0 = std::chrono::steady_clock::now();
         std::vector<std::thread> th;
@@ -78,28 +79,42 @@ int main() {
                 for (int c : doms[(size_t)t % doms.size()]) CPU_SET(c, &set);
                 pthread_setaffinity_np(pthread_self(), sizeof set, &set);
             }
-            // pieces of `piece` pixels (a chunk, or a bin's row of 6 chunks), in an order that jumps
-            // between rows like bins do; the frame 16 B into its first line, as a malloc'd buffer
+            // pieces of `piece` pixels (a chunk, a bin's row of 6 chunks, or a whole bin staged
+            // contiguously), in an order that jumps between rows like bins do -- or, with `blocks`, the
+            // host fill's own order (thread t takes blocks t, t + T, ... of 8 consecutive pieces); the
+            // frame 16 B into its first line, as a malloc'd buffer
             const size_t chunks = npx / piece - 1;
-            for (size_t k = t; k < chunks; k += T) {
-                const size_t c = (k * 2654435761ull) % chunks;
-                widen(stage + 3 * piece * c, frame + 4 + piece * c, piece);
+            if (blocks) {
+                for (size_t b0 = 8 * t; b0 < chunks; b0 += 8 * T)
+                    for (size_t c = b0; c < b0 + 8 && c < chunks; c++) widen(stage + 3 * piece * c, frame + 4 + piece * c, piece);
+            } else {
+                for (size_t k = t; k < chunks; k += T) {
+                    const size_t c = (k * 2654435761ull) % chunks;
+                    widen(stage + 3 * piece * c, frame + 4 + piece * c, piece);
+                }
             }
             _mm_sfence();
         });
         for (auto &x : th) x.join();
-        printf("%-40s %8.1f us\n", what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        printf("%-48s T=%d %8.1f us\n", what, T, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     };
     (void)W;
-    for (size_t pc : {64, 384}) {
-        piece = pc;
-        printf("pieces of %zu px\n", pc);
-        for (int rep = 0; rep < 2; rep++) {
-            memset(stage, rep, npx * 3);
-            run_widen("widen, staging written by the CPU");
-            hipLaunchKernelGGL(k_stage, dim3(1024), dim3(256), 0, nullptr, sdev, npx * 3 / 4, (unsigned)rep);
-            CK(hipDeviceSynchronize());
-            run_widen("widen, staging written by the GPU");
+    for (int bl = 0; bl < 2; bl++) {
+        blocks = bl == 1;
+        for (size_t pc : {64, 384, 1536}) {
+            if (blocks && pc != 1536) continue;
+            piece = pc;
+            for (int tt : {4, 8}) {
+                T = tt;
+                printf("pieces of %zu px%s\n", pc, blocks ? ", blocks of 8 in thread order" : ", hashed order");
+                for (int rep = 0; rep < 2; rep++) {
+                    memset(stage, rep, npx * 3);
+                    run_widen("widen, staging written by the CPU");
+                    hipLaunchKernelGGL(k_stage, dim3(1024), dim3(256), 0, nullptr, sdev, npx * 3 / 4, (unsigned)rep);
+                    CK(hipDeviceSynchronize());
+                    run_widen("widen, staging written by the GPU");
+                }
+            }
         }
     }
     return 0;
