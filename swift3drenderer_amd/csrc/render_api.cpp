@@ -74,7 +74,7 @@ constexpr int kSets = 4;
 #define S3R_GEO_STREAMS 2
 #endif
 constexpr int kGeoStreams = S3R_GEO_STREAMS;
-constexpr uint64_t kLptMinBins = 4000;      // longest-first fragment order from this many bins (~3 rounds; see render_core)
+constexpr uint64_t kLptMinBins = 2000;      // longest-first fragment order from this many bins (~1.5 rounds; see render_core)
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
 // the order-independent tile path takes over (the icosahedron stress scene).
 constexpr uint64_t kRowPathMaxSlots = 8192;
@@ -1100,8 +1100,11 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
         HIPCHECK(hipDeviceSynchronize());
         d.bins_cap = nbins;
     }
-    // longest-first order only where a launch is several rounds of resident workgroups (~1 280 on
-    // the chip): a frame part of one round gains nothing and would pay the order column's time
+    // longest-first order only where a launch is more than one round of resident workgroups (~1 280
+    // on the chip): a frame part of one round gains nothing and would pay the order column's time.
+    // Round 4 (tools/lpt_sweep.sh, two repeats): 2 000 instead of 4 000 bins puts part 0 of 8 of the
+    // 8K frame (2 700 bins) on it, 27 100-27 200 -> 29 400-29 500 fps; 4K part 0 of 8 (2 040 bins) and
+    // 1080p (flat) move by <= 0.3 %
     const uint64_t bins = nbins;
     const char *lpt_env = getenv("S3R_LPT_MIN");            // tuning / test override
     // (delivered frames are bound by the link, not by their heaviest bins: launch order, no order

@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_gputest.log 2>&1
+rc=$?; tail -5 gpurun_out/r04_gputest.log; exit $rc
