@@ -2104,7 +2104,7 @@ __global__ void __launch_bounds__(256) k_tile_cursor(uint32_t *__restrict__ coun
         if (threadIdx.x == 0) {
             const uint32_t total = offs[n - 1u] + counts[n - 1u];
             if (n - 1u >= 256u) counts[n - 1u] = 0u;       // (its own workgroup leaves it to this one)
-            ctr[0] = lv; ctr[1] = total; ctr[2] = kept;
+            ctr[0] = lv; ctr[1] = total; ctr[2] = kept; ctr[3] = 0u;
             if (sum_host) {
                 __hip_atomic_store(sum_host + 1, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(sum_host + 2, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2182,10 +2182,74 @@ __device__ __forceinline__ void slot_setup(uint32_t s, uint32_t ntri, const floa
     setup_tri(d, textured, sw, sh, &out);
 }
 
+// The scene and camera a tile-path pixel is shaded from (k_tile_resolve, the fused raster).
+struct ShadeScene {
+    const RasterRec *recs;
+    const float4 *vtx, *nrm, *pay;
+    const uint8_t *disc;
+    const uint32_t *vidx, *aidx, *tex;
+    uint32_t ntri, ntex;
+    Mat34 m;
+    float factor, sw, sh;
+};
+constexpr uint32_t kDeferPixel = 0xFFFFFFFFu;           // (never a pixel: 0x00RRGGBB)
+
+// The pixel (x, frame row y) of winner key k (render.cpp:360-373 for the winner; background where no
+// fragment): the winner re-walked exactly from its raster record and shaded with constants
+// recomputed from the scene.  An unclipped winner takes its 1/z and steps from its record (the
+// values k_tile_setup computed); a clip-appended or near-plane-crossing winner needs its full setup
+// (slot_setup, the clip) -- with DEFER the pixel returns kDeferPixel for k_tile_resolve_deferred
+// instead (rare, and the clip's registers stay out of the caller).
+template <bool DEFER>
+__device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned long long k, uint32_t x, uint32_t y) {
+    if (!k) return kBackground;
+    const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
+    const float ooz = u2f((uint32_t)(k >> 32));
+    if (DEFER && s >= sc.ntri) return kDeferPixel;
+    const float4 *q = reinterpret_cast<const float4 *>(sc.recs + s);
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
+    const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
+    const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
+    const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
+    TriSetup ts;
+    const uint32_t t = s < sc.ntri ? s : s - sc.ntri;
+    Vert d[3];
+    bool near_cut = false;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const uint32_t ai = sc.aidx[3 * t + c];
+        const F3 cv = mat_mul(sc.m, sc.vtx[sc.vidx[3 * t + c]]);
+        const float nz = -cv.z;
+        d[c].cv = cv;
+        d[c].rv = mk3(0.0f, 0.0f, (0.0f * sc.factor) / nz + nz);               // :288 (z only)
+        d[c].n = mat_mul(sc.m, sc.nrm[ai]);
+        d[c].pay = sc.pay[ai];
+        near_cut = near_cut || d[c].rv.z < kNear;
+    }
+    if (s >= sc.ntri || near_cut) {
+        if (DEFER) return kDeferPixel;
+        slot_setup(s, sc.ntri, sc.vtx, sc.nrm, sc.pay, sc.disc, sc.vidx, sc.aidx, sc.m, sc.factor, sc.sw, sc.sh, ts);
+    } else {
+        ts.kind = kDead;
+        ts.rvz[0] = q3.y; ts.rvz[1] = q3.z; ts.rvz[2] = q3.w;
+        ts.dx[0] = q1.w; ts.dx[1] = q2.x; ts.dx[2] = q2.y;
+        ts.dy[0] = q2.z; ts.dy[1] = q2.w; ts.dy[2] = q3.x;
+        shading_part(d, sc.disc[sc.aidx[3 * t]] != 0, ts);
+    }
+    return shade(&ts, w0, w1, w2, ooz, sc.tex, sc.ntex);
+}
+
+// FUSED: the tile's winners are shaded here, straight from LDS, and stored to out (its local row, or
+// with frame_rows its frame row) -- no per-pixel key round trip through HBM and, for frames written
+// into the caller's buffer, each tile's stores cross the link while other tiles rasterize; pixels
+// whose winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).
+template <bool FUSED>
 __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
-    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0) {
+    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0,
+    ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred) {
     __shared__ TileShared ls;
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
@@ -2391,10 +2455,39 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     }
 #endif
     __syncthreads();
+    if (FUSED) {
+        for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {   // (wave-uniform trip count)
+            const uint32_t rr = i / kTileW, cc = i % kTileW;
+            const uint32_t lr = tr0 + rr, x = lx0 + cc;
+            const bool in = lr <= tr1 && x <= lx1;
+            const unsigned long long k = in ? ls.key[rr * kKeyStride + cc] : 0ull;
+            const uint32_t y = row_of(lr);
+            uint32_t v = kBackground;
+            if (in) v = resolve_pixel<true>(sc, k, x, y);
+            const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
+            wave_append(in && v == kDeferPixel, make_uint4((uint32_t)idx, (uint32_t)k, (uint32_t)(k >> 32), (x & 0xFFFFu) | (y << 16)),
+                        deferred, ctr + 3);
+            if (in && v != kDeferPixel) out[idx] = v;
+        }
+        return;
+    }
     for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {
         const uint32_t rr = i / kTileW, cc = i % kTileW;
         const uint32_t lr = tr0 + rr, x = lx0 + cc;
         if (lr <= tr1 && x <= lx1) keys[(size_t)lr * W + x] = ls.key[rr * kKeyStride + cc];
+    }
+}
+
+// The fused raster's deferred pixels (ctr[3] entries {out index, key, x | y << 16}): shaded with the
+// winner's full setup.  Grid-stride (the queue is short: pixels of near-plane and clip-appended
+// winners).
+__global__ void __launch_bounds__(256) k_tile_resolve_deferred(ShadeScene sc, const uint4 *__restrict__ deferred,
+                                                               const uint32_t *__restrict__ ctr, uint32_t *__restrict__ out) {
+    const uint32_t n = ctr[3];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint4 e = deferred[i];
+        const unsigned long long k = (unsigned long long)e.y | ((unsigned long long)e.z << 32);
+        out[e.x] = resolve_pixel<false>(sc, k, e.w & 0xFFFFu, e.w >> 16);
     }
 }
 
@@ -2417,46 +2510,8 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
     if (frame_rows == 2u) x -= (uint32_t)(((uintptr_t)(out + (size_t)y * W)) >> 2) & 15u;
     if (x >= W) return;                                // (x wrapped below 0 included)
     const size_t idx = (size_t)lr * W + x;
-    const unsigned long long k = keys[idx];
-    uint32_t v = kBackground;
-    if (k) {
-        const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
-        const float ooz = u2f((uint32_t)(k >> 32));
-        const float4 *q = reinterpret_cast<const float4 *>(recs + s);
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-        const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
-        const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
-        const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
-        const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
-        TriSetup ts;
-        // the winner's shading constants: corners transformed again (render.cpp:286, :291); an
-        // unclipped triangle takes its 1/z and steps from its raster record (the same values
-        // k_tile_setup computed), a clipped one is set up in full
-        const uint32_t t = s < ntri ? s : s - ntri;
-        Vert d[3];
-        bool near_cut = false;
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const uint32_t ai = aidx[3 * t + c];
-            const F3 cv = mat_mul(m, vtx[vidx[3 * t + c]]);
-            const float nz = -cv.z;
-            d[c].cv = cv;
-            d[c].rv = mk3(0.0f, 0.0f, (0.0f * factor) / nz + nz);                 // :288 (z only)
-            d[c].n = mat_mul(m, nrm[ai]);
-            d[c].pay = pay[ai];
-            near_cut = near_cut || d[c].rv.z < kNear;
-        }
-        if (s >= ntri || near_cut) {
-            slot_setup(s, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, sw, sh, ts);
-        } else {
-            ts.kind = kDead;
-            ts.rvz[0] = q3.y; ts.rvz[1] = q3.z; ts.rvz[2] = q3.w;
-            ts.dx[0] = q1.w; ts.dx[1] = q2.x; ts.dx[2] = q2.y;
-            ts.dy[0] = q2.z; ts.dy[1] = q2.w; ts.dy[2] = q3.x;
-            shading_part(d, disc[aidx[3 * t]] != 0, ts);
-        }
-        v = shade(&ts, w0, w1, w2, ooz, tex, ntex);
-    }
+    const ShadeScene sc{recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
+    const uint32_t v = resolve_pixel<false>(sc, keys[idx], x, y);
     out[frame_rows ? (size_t)y * W + x : idx] = v;      // (frame_rows: the caller's mapped frame)
 }
 
@@ -2892,9 +2947,27 @@ void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t np
     const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
     ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
     if (tx == 0 || ty0 >= ty1) return;
-    hipLaunchKernelGGL(k_tile_raster, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
+    const ShadeScene none{};
+    hipLaunchKernelGGL(k_tile_raster<false>, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
                        band, nparts, part, rows_local, tx, offs, ctr, list, keys,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx);
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx, none, (uint32_t *)nullptr, 0u,
+                       (uint4 *)nullptr);
+}
+
+void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
+                                const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
+                                const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
+                                uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                                uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
+                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows) {
+    const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
+    if (tx == 0 || ty == 0) return;
+    const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
+    hipLaunchKernelGGL(k_tile_raster<true>, dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band,
+                       nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr,
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred);
+    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred,
+                       (const uint32_t *)ctr, out);
 }
 
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,

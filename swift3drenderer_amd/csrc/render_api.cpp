@@ -139,6 +139,8 @@ struct Dev {
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
     size_t keys_cap = 0;
+    uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
+    size_t deferred_cap = 0;
     // host-coherent, per buffer set: {tag, live entries, list length, cluster-kept positions}, written
     // by k_tile_cursor as soon as they are known (tag = the frame's number)
     uint32_t *tile_sum_host = nullptr, *tile_sum_dev = nullptr;
@@ -334,6 +336,8 @@ struct Lib {
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
+    int tile_fused = -1;                       // tile path: raster and resolve in one launch (S3R_TILE_FUSED:
+                                               // -1 whole frames only, the default; 0 never; 1 always)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -627,6 +631,8 @@ void initialize() {
         g.tile_slabs = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
         const char *l = getenv("S3R_TILE_LINE");
         g.tile_line_grid = !(l && atoi(l) == 0);
+        const char *f = getenv("S3R_TILE_FUSED");
+        g.tile_fused = f ? (atoi(f) != 0 ? 1 : 0) : -1;
     }
     for (int id : ids) {
         Dev *d = new Dev();
@@ -662,7 +668,7 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.scan_temp, d.vrv, d.geo_cnt,
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
                     d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -871,7 +877,23 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     const uint32_t th = tile_height(), tyn = (rows_local + th - 1) / th;
     uint32_t slabs = frame_rows ? g.tile_slabs : 1u;
     slabs = std::max(1u, std::min({slabs, tyn, kMaxTileSlabs}));
-    if (slabs == 1u) {
+    // fused raster + resolve: whole frames by default -- stress scene, one MI355X
+    // (profiles/r04_tile_fused_ab.txt): whole frame 800 -> 854 fps in HBM, delivered 583 -> 614; part 0
+    // of 8 4 328 -> 4 026 (its longer-lived workgroups hold slots the next frame's setup, the part's
+    // bound, runs in)
+    const bool fused = g.tile_fused == 1 || (g.tile_fused < 0 && nparts == 1);
+    if (fused) {
+        const size_t npx = (size_t)W * rows_local;
+        if (d.deferred_cap < npx) {
+            HIPCHECK(hipDeviceSynchronize());
+            if (d.deferred) HIPCHECK(hipFree(d.deferred));
+            d.deferred = dalloc<uint4>(npx);
+            d.deferred_cap = npx;
+        }
+        launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                                   d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
+                                   d.tile_list[p], d.tile_list_cap[p], d.deferred, st, frame_rows);
+    } else if (slabs == 1u) {
         launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], d.tile_list[p],
                            d.keys, d.tile_list_cap[p], st);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,

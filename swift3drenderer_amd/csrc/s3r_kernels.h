@@ -113,7 +113,8 @@ constexpr uint32_t kTileShards = 64, kTileShardStride = 64;
 std::vector<uint32_t> cluster_shard_table(const std::vector<uint32_t> &first);
 // ctr: kTileCtrWords device words per buffer set (allocate them zeroed; the tile kernels leave the
 // shard counters zero again after each frame): [0] live entries, [1] the
-// tile lists' total length, [2] positions the cluster cull kept (the first kTileCounterWords are
+// tile lists' total length, [2] positions the cluster cull kept, [3] the fused raster's deferred
+// pixels (the first kTileCounterWords are
 // the summary the host reads back), then the shards' counters.  live: 2T entries (tile box, rows,
 // slot, 0); clipq: T words (the positions whose triangle crosses the near plane).  cl (may be null
 // or empty): cull clusters first and set up only their triangles; vrv (nv float4, may be null;
@@ -146,6 +147,15 @@ void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t np
                         uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                         unsigned long long *keys, uint64_t cap, hipStream_t st,
                         uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu);   // tile rows [ty0, ty1) only
+// Raster and resolve in one launch (each tile shades its winners from LDS and stores them into out:
+// its local rows, or with frame_rows the frame rows of a W x H frame), then the pixels whose winner
+// needs a full setup (ctr[3] of them, in `deferred`: W x rows_local entries) in a second, short one.
+void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
+                                const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
+                                const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
+                                uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
+                                uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
+                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows);
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,

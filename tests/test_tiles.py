@@ -335,10 +335,12 @@ def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, de
     stream while slab k + 1 rasterizes) equal the oracle's, for slab counts that divide the tile rows
     unevenly or exceed them, frame heights that end inside a tile, and two parts; with the resolve's
     waves on the caller's 64-B line grid (S3R_TILE_LINE=1, the default: rows starting mid-line, an
-    odd width) and without."""
+    odd width) and without.  The split raster / resolve launches (S3R_TILE_FUSED=0; whole frames are
+    fused by default)."""
     from oracle.oracle import OracleRenderer
     monkeypatch.setenv('S3R_TILE_SLABS', slabs)
     monkeypatch.setenv('S3R_TILE_LINE', line)
+    monkeypatch.setenv('S3R_TILE_FUSED', '0')          # (the slabs are the split raster / resolve's)
     r = gpu_renderer
     r.configure_devices(devices)
     path = icosa_dir[2000]
@@ -359,3 +361,35 @@ def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, de
     finally:
         r.set_delivery('env')
         r.configure_devices([])
+
+
+@pytest.mark.parametrize('case', [('full', 'P_clip', 640, 480, 1), ('full', 'P_over', 1000, 333, 1),
+                                  ('stress', 'P_id', 1920, 1080, 1), ('stress', 'P_strafe', 1280, 720, 3)])
+def test_fused_raster_resolve_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeypatch, case):
+    """Raster and resolve in one launch (S3R_TILE_FUSED=1): each tile shades its winners from LDS;
+    pixels whose winner was clipped at the near plane (P_clip) go through the deferred pass.  Whole
+    frames, a 3-part split, and direct delivery into the caller's buffer."""
+    import torch
+    from swift3drenderer_amd.multi import assemble
+    monkeypatch.setenv('S3R_TILE_FUSED', '1')
+    name, pose, w, h, nparts = case
+    path = icosa_dir[2000] if name == 'stress' else scene_dir[name]
+    r = gpu_renderer
+    r.set_raster_path('tiles')
+    try:
+        script = poses.script(pose)
+        want = oracle_render_pose(path, script, w, h, extra_frames=1)
+        got = render_pose(r, path, script, w, h, extra_frames=1)     # updateAndRender: direct delivery
+        assert np.array_equal(got, want), diff(got, want)
+        inp = (0, 0, 0, 0) + tuple(script[-1][4:6])
+        parts = []
+        for part in range(nparts):
+            rows = r.lib.s3r_band_rows_local(h, 16 if nparts > 1 else h, nparts, part)
+            buf = torch.empty((rows, w), dtype=torch.int32, device='cuda')
+            r.render_bands(inp, w, h, 16 if nparts > 1 else h, nparts, part, buf.data_ptr(), 0)
+            torch.cuda.synchronize()
+            parts.append(buf.cpu().numpy().view(np.uint32))
+        got = assemble(parts, h, 16) if nparts > 1 else parts[0]
+        assert np.array_equal(got, want), diff(got, want)
+    finally:
+        r.set_raster_path('auto')
