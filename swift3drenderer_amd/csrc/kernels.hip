@@ -2492,13 +2492,15 @@ __global__ void __launch_bounds__(256) k_tile_resolve_deferred(ShadeScene sc, co
 }
 
 // One thread per pixel: the winner of each pixel (key), re-walked exactly from its raster record
-// and shaded with constants recomputed from the scene (slot_setup); background where no fragment.
+// and shaded with constants recomputed from the scene (resolve_pixel); background where no fragment;
+// a pixel whose winner needs its full setup (clip) is queued for k_tile_resolve_deferred.
 __global__ void __launch_bounds__(256) k_tile_resolve(
     const unsigned long long *__restrict__ keys, const RasterRec *__restrict__ recs, const float4 *__restrict__ vtx,
     const float4 *__restrict__ nrm, const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
     const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
     float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
-    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows, uint32_t by0) {
+    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows, uint32_t by0,
+    uint4 *__restrict__ deferred, uint32_t *__restrict__ ctr) {
     const uint32_t lr = (by0 + blockIdx.y) * 4u + (threadIdx.x >> 6);
     if (lr >= rows_local) return;
     const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
@@ -2508,11 +2510,16 @@ __global__ void __launch_bounds__(256) k_tile_resolve(
     // store crosses the link as four whole lines instead of five partly written ones
     uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
     if (frame_rows == 2u) x -= (uint32_t)(((uintptr_t)(out + (size_t)y * W)) >> 2) & 15u;
-    if (x >= W) return;                                // (x wrapped below 0 included)
+    const bool in = x < W;                             // (x wrapped below 0 included)
     const size_t idx = (size_t)lr * W + x;
     const ShadeScene sc{recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
-    const uint32_t v = resolve_pixel<false>(sc, keys[idx], x, y);
-    out[frame_rows ? (size_t)y * W + x : idx] = v;      // (frame_rows: the caller's mapped frame)
+    const unsigned long long k = in ? keys[idx] : 0ull;
+    const uint32_t v = in ? resolve_pixel<true>(sc, k, x, y) : kBackground;
+    const size_t o = frame_rows ? (size_t)y * W + x : idx;   // (frame_rows: the caller's mapped frame)
+    // a winner that needs its full setup: the pixel goes to k_tile_resolve_deferred
+    wave_append(in && v == kDeferPixel, make_uint4((uint32_t)o, (uint32_t)k, (uint32_t)(k >> 32), (x & 0xFFFFu) | (y << 16)),
+                deferred, ctr + 3);
+    if (in && v != kDeferPixel) out[o] = v;
 }
 
 // ------------------------------------------------------------------ self-test kernel
@@ -2975,13 +2982,21 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                          uint32_t rows_local, hipStream_t st, bool frame_rows, uint32_t r0, uint32_t r1,
-                         bool line_grid) {
+                         bool line_grid, uint4 *deferred, uint32_t *ctr) {
     r1 = std::min(r1, rows_local);
     if (W == 0 || r0 >= r1 || (r0 & 3u)) return;
     const uint32_t mode = frame_rows ? (line_grid ? 2u : 1u) : 0u;
     hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64 + (mode == 2u ? 1u : 0u), (r1 - r0 + 3) / 4), dim3(256), 0,
                        st, keys, (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex,
-                       ntex, out, W, band, nparts, part, r1, mode, r0 / 4u);
+                       ntex, out, W, band, nparts, part, r1, mode, r0 / 4u, deferred, ctr);
+}
+
+void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
+                                  const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
+                                  const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
+                                  uint32_t *out, const uint4 *deferred, const uint32_t *ctr, hipStream_t st) {
+    const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
+    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, deferred, ctr, out);
 }
 
 }  // namespace s3r

@@ -882,14 +882,14 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     // of 8 4 328 -> 4 026 (its longer-lived workgroups hold slots the next frame's setup, the part's
     // bound, runs in)
     const bool fused = g.tile_fused == 1 || (g.tile_fused < 0 && nparts == 1);
+    const size_t npx = (size_t)W * rows_local;
+    if (d.deferred_cap < npx) {                // pixels whose winner needs its full setup (either way)
+        HIPCHECK(hipDeviceSynchronize());
+        if (d.deferred) HIPCHECK(hipFree(d.deferred));
+        d.deferred = dalloc<uint4>(npx);
+        d.deferred_cap = npx;
+    }
     if (fused) {
-        const size_t npx = (size_t)W * rows_local;
-        if (d.deferred_cap < npx) {
-            HIPCHECK(hipDeviceSynchronize());
-            if (d.deferred) HIPCHECK(hipFree(d.deferred));
-            d.deferred = dalloc<uint4>(npx);
-            d.deferred_cap = npx;
-        }
         launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                    d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
                                    d.tile_list[p], d.tile_list_cap[p], d.deferred, st, frame_rows);
@@ -898,7 +898,9 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                            d.keys, d.tile_list_cap[p], st);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
                             sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
-                            g.tile_line_grid);
+                            g.tile_line_grid, d.deferred, d.tile_ctr[p]);
+        launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], st);
     } else {
         if (!d.res_stream) {
             HIPCHECK(hipSetDevice(d.device));
@@ -914,8 +916,10 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
             HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
             launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
                                 sw, sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.res_stream, frame_rows,
-                                ty0 * th, std::min(rows_local, ty1 * th), g.tile_line_grid);
+                                ty0 * th, std::min(rows_local, ty1 * th), g.tile_line_grid, d.deferred, d.tile_ctr[p]);
         }
+        launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], d.res_stream);
         HIPCHECK(hipEventRecord(d.res_done, d.res_stream));
         HIPCHECK(hipStreamWaitEvent(st, d.res_done, 0));
     }

@@ -160,9 +160,15 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
                          uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows = false,
-                         uint32_t r0 = 0, uint32_t r1 = 0xFFFFFFFFu,      // local rows [r0, r1) only (r0 % 4 == 0)
-                         bool line_grid = false);   // frame_rows: wave stores on the caller's 64-B line grid
+                         uint32_t rows_local, hipStream_t st, bool frame_rows,
+                         uint32_t r0, uint32_t r1,           // local rows [r0, r1) only (r0 % 4 == 0)
+                         bool line_grid,                     // frame_rows: wave stores on the caller's 64-B line grid
+                         uint4 *deferred, uint32_t *ctr);    // pixels whose winner needs its full setup (ctr[3])
+// Those pixels, shaded with the winner's full setup (after every resolve launch of the frame).
+void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
+                                  const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
+                                  const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
+                                  uint32_t *out, const uint4 *deferred, const uint32_t *ctr, hipStream_t st);   // frame_rows: wave stores on the caller's 64-B line grid
 
 // The N parts of an interleaved band split, gathered one after another (part p's compact rows from
 // row p * part_stride_rows), written into the W x H frame in frame-row order (one launch).
