@@ -194,6 +194,13 @@ uint32_t s3r_device_profile(uint64_t *out, uint32_t max_devices);
  * every triangle). */
 void s3r_cluster_stats(uint64_t out[4]);
 
+/* Test hook, no GPU needed: the tile path's upper bound of every 1/z a triangle with this raster
+ * setup (render.cpp:319-336: ws, per-pixel steps dx, per-row steps dy, 1/z per corner, bbox) can
+ * produce at a pixel it covers, as the kernels compute it (k_tile_raster skips a triangle whose bound
+ * is below every current winner of the rows it meets). */
+float s3r_ooz_bound(const float ws[3], const float dx[3], const float dy[3], const float rvz[3], uint32_t xmin,
+                    uint32_t xmax, uint32_t ymin, uint32_t ymax);
+
 /* Test hook, no GPU needed: the clusters the library builds for a vertex list (nv x float4) and
  * index list (3 ntri vertex indices < nv).  Returns the cluster count C; writes the first
  * min(C + 1, first_cap) position-range starts to first_out, min(C, first_cap) bounding spheres

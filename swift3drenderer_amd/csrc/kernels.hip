@@ -1721,8 +1721,12 @@ static_assert(kDepthBuckets <= 64, "bucket field of a packed tile box");
 // the same key share one atomic.  With `list`, the returned positions place `slot` in the lists.
 // Per step the groups are found first (ballots only), then every group leader issues its atomic in
 // ONE vector instruction, so a step waits for one atomic round trip, not one per distinct tile.
+// With `stride` (bins mode), counter[key] counts key's entries and entry i of key goes to
+// list[key * stride + i] directly (no scan, no fill pass); an entry past stride is dropped and
+// *ovf raised to the count key needs (the frame is then binned again, render_api.cpp).
 __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x, uint32_t *__restrict__ ctr,
-                                           uint32_t *__restrict__ list, uint32_t slot, uint32_t cap = 0xFFFFFFFFu) {
+                                           uint32_t *__restrict__ list, uint32_t slot, uint32_t cap = 0xFFFFFFFFu,
+                                           uint32_t stride = 0, uint32_t *__restrict__ ovf = nullptr) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t rounds = sp.n;
     for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
@@ -1759,7 +1763,14 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
 #pragma unroll
             for (uint32_t q = 0; q < kSteps; q++) {
                 const uint32_t b = (uint32_t)__shfl((int)base[q], (int)leader_of[q]);
-                if (k0 + q < sp.n && b + rank[q] < cap) list[b + rank[q]] = slot;   // (past cap: overflow)
+                if (stride) {
+                    if (k0 + q < sp.n) {
+                        if (b + rank[q] < stride) list[(size_t)key[q] * stride + b + rank[q]] = slot;
+                        else atomicMax(ovf, b + rank[q] + 1u);
+                    }
+                } else if (k0 + q < sp.n && b + rank[q] < cap) {
+                    list[b + rank[q]] = slot;                                  // (past cap: overflow)
+                }
             }
         }
     }
@@ -1776,7 +1787,7 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
 // A_i), the sum's by 2^-20 (|S| + slack), the product's by the final 2^-18.  A pixel whose current
 // winner has a larger 1/z cannot be won by this triangle (strict '>' at :364), so k_tile_raster may
 // skip it.
-__device__ float ooz_bound(const TriSetup &t) {
+S3R_HD float ooz_bound(const TriSetup &t) {
     const float nx = (float)(t.xmax - t.xmin), ny = (float)(t.ymax - t.ymin);   // (exact: < 2^16)
     float S = -__builtin_inff(), sumA = 0.0f, Amax = 0.0f;
 #pragma unroll
@@ -1936,10 +1947,13 @@ __device__ __forceinline__ void wave_append_u32(bool want, uint32_t v, uint32_t 
 // A live slot's raster record, live entry and (tile, bucket) counts -- or nothing when its box misses
 // this part's rows (row-band split: the slot is dead here).  Every lane of the wave calls it (the
 // entry append and the counting are wave-aggregated).
+// Bins mode (tbin non-null, kernels.hip "bins"): the slot goes straight into the fixed-capacity
+// bins of its (tile, bucket)s -- no live entry, no fill pass.
 __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_t slot, uint32_t band, uint32_t nparts,
                                           uint32_t part, uint32_t tiles_x, RasterRec *__restrict__ recs,
                                           uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
-                                          uint32_t *__restrict__ counts) {
+                                          uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin = nullptr,
+                                          uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr) {
     uint32_t bx = kDeadBox, by = 0;
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
@@ -1951,6 +1965,10 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
             by = ts.ymin | (ts.ymax << 16);
             write_rec(recs + slot, ts, slot, zb);
         }
+    }
+    if (tbin) {
+        tile_visit(sp, tiles_x, counts, tbin, slot, 0xFFFFFFFFu, bin_cap, ovf);
+        return;
     }
     wave_append(bx != kDeadBox, make_uint4(bx, by, slot, 0), lv, nlive);
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 1)
@@ -1976,7 +1994,8 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
                                                     uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                     RasterRec *__restrict__ recs, uint4 *__restrict__ live,
                                                     uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
-                                                    uint32_t *__restrict__ counts, const float4 *__restrict__ vrv) {
+                                                    uint32_t *__restrict__ counts, const float4 *__restrict__ vrv,
+                                                    uint32_t *__restrict__ tbin, uint32_t bin_cap) {
     const uint32_t lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards, rank = blockIdx.x / kTileShards;
     const uint32_t per = gridDim.x / kTileShards;              // workgroups per shard (launch: a multiple)
     const uint32_t b0 = shard_base(CL ? shard_tab : nullptr, ntri, sh_id);
@@ -2028,7 +2047,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -2044,7 +2063,8 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
                                                    RasterRec *__restrict__ recs, uint4 *__restrict__ live,
                                                    const uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
-                                                   uint32_t *__restrict__ counts) {
+                                                   uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin,
+                                                   uint32_t bin_cap) {
     const uint32_t lane = threadIdx.x & 63u, sh_id = blockIdx.x % kTileShards, rank = blockIdx.x / kTileShards;
     const uint32_t per = gridDim.x / kTileShards;
     const uint32_t b0 = shard_base(CL ? shard_tab : nullptr, ntri, sh_id);
@@ -2075,8 +2095,8 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
             if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) live_a = raster_part(app, sw, sh, ta);
             live_t = raster_part(d, sw, sh, ts);
         }
-        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts);
+        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -2117,6 +2137,33 @@ __global__ void __launch_bounds__(256) k_tile_cursor(uint32_t *__restrict__ coun
     if (i >= n) return;
     cursor[i] = offs[i];
     if (first && (i != n - 1u || blockIdx.x == 0)) counts[i] = 0u;
+}
+
+// Bins mode's end of binning (in place of the scan, the cursors and the fill): the summary -- ctr[2]
+// the positions the cluster cull kept, ctr[5] = the count an overflowing (tile, bucket) needs (0: none,
+// k_tile_raster renders nothing then) from the setup's ctr[4], which it resets -- to ctr and, when
+// sum_host is given, {tag, 0, 0, kept, needed} to the host (tag last); the shards' cull and clip
+// counters reset for the set's next frame.
+__global__ void __launch_bounds__(64) k_tile_bins_done(uint32_t *__restrict__ ctr, uint32_t *__restrict__ sum_host,
+                                                       uint32_t tag) {
+    static_assert(kTileShards == 64, "one lane per shard");
+    const uint32_t t = threadIdx.x;
+    uint32_t kept = *shard_ctr(ctr, 0, t);
+    *shard_ctr(ctr, 0, t) = 0u;
+    *shard_ctr(ctr, 2, t) = 0u;
+    for (int o = 32; o > 0; o >>= 1) kept += (uint32_t)__shfl_xor((int)kept, o);
+    if (t == 0) {
+        const uint32_t need = ctr[4];
+        ctr[4] = 0u;
+        ctr[0] = 0u; ctr[1] = 0u; ctr[2] = kept; ctr[3] = 0u; ctr[5] = need;
+        if (sum_host) {
+            __hip_atomic_store(sum_host + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(sum_host + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(sum_host + 3, kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(sum_host + 4, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(sum_host, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // Scatter: workgroup b serves shard b % kTileShards, grid-stride over its live entries (original and
@@ -2249,7 +2296,8 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
     const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0,
-    ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred) {
+    ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred,
+    uint32_t *__restrict__ counts, uint32_t bin_cap) {
     __shared__ TileShared ls;
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
@@ -2268,18 +2316,48 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     for (uint32_t i = tid; i < kTileH * kKeyStride; i += kTileThreads) ls.key[i] = 0ull;
     // the tile's list: its depth buckets, nearest first, one after another
     const uint32_t s0 = tile * kDepthBuckets;
-    // a list longer than its buffer (overflow, see k_tile_fill) is incomplete: the frame is redone
-    const uint32_t ntiles = tiles_x * ((rows_local + kTileH - 1u) / kTileH);
-    const uint32_t end = tile + 1u < ntiles ? offs[s0 + kDepthBuckets] : *total;
-    const uint32_t base = offs[s0], n = *total > cap ? 0u : end - base;
-    if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
+    uint32_t base = 0, n = 0;
+    if (bin_cap) {
+        // bins mode: bucket b's entries at list[(s0 + b) * bin_cap ...], counts[s0 + b] of them; the
+        // counts reset for the set's next frame once read.  An overflowed frame (ctr[5]) renders
+        // nothing: it is binned again with larger bins (render_api.cpp)
+        if (tid < 64u) {
+            const uint32_t c = tid < kDepthBuckets ? counts[s0 + tid] : 0u;
+            if (tid < kDepthBuckets) counts[s0 + tid] = 0u;
+            uint32_t inc = c;
+            for (uint32_t o = 1; o < 64u; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
+                if (tid >= o) inc += v;
+            }
+            if (tid < kDepthBuckets) ls.bstart[tid] = inc - c;
+            if (tid == 63u) ls.zwave[0] = ctr[5] ? 0u : inc;       // (zwave: free until the first stage)
+        }
+        __syncthreads();
+        n = ls.zwave[0];
+    } else {
+        // a list longer than its buffer (overflow, see k_tile_fill) is incomplete: the frame is redone
+        const uint32_t ntiles = tiles_x * ((rows_local + kTileH - 1u) / kTileH);
+        const uint32_t end = tile + 1u < ntiles ? offs[s0 + kDepthBuckets] : *total;
+        base = offs[s0];
+        n = *total > cap ? 0u : end - base;
+        if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
+    }
     // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
     // while stage c0's items run
     uint32_t s_nx = 0;
     float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n, q3n = q0n;
     auto fetch = [&](uint32_t c) {
         if (tid < kTileStage && c + tid < n) {
-            s_nx = list[base + c + tid];
+            if (bin_cap) {
+                const uint32_t v = c + tid;
+                uint32_t b = 0;                                  // the bucket holding entry v
+#pragma unroll
+                for (uint32_t step = 16; step >= 1u; step >>= 1)
+                    if (ls.bstart[b + step] <= v) b += step;
+                s_nx = list[(size_t)(s0 + b) * bin_cap + (v - ls.bstart[b])];
+            } else {
+                s_nx = list[base + c + tid];
+            }
             const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
             q0n = q[0]; q1n = q[1]; q2n = q[2]; q3n = q[3];
         }
@@ -2834,6 +2912,16 @@ void launch_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_ro
                            nparts, frame);
 }
 
+// Test hook (include/render.h s3r_ooz_bound): the tile path's 1/z bound of a raster setup, computed
+// on the host by the same code the kernels run.
+float ooz_bound_host(const float ws[3], const float dx[3], const float dy[3], const float rvz[3], uint32_t xmin,
+                     uint32_t xmax, uint32_t ymin, uint32_t ymax) {
+    TriSetup t{};
+    for (int i = 0; i < 3; i++) { t.ws[i] = ws[i]; t.dx[i] = dx[i]; t.dy[i] = dy[i]; t.rvz[i] = rvz[i]; }
+    t.xmin = xmin; t.xmax = xmax; t.ymin = ymin; t.ymax = ymax;
+    return ooz_bound(t);
+}
+
 uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
 uint32_t tile_height() { return kTileH; }
 static_assert(kTileH % 4u == 0, "tile rows = whole 4-row resolve blocks (slabbed fragment stage)");
@@ -2890,21 +2978,23 @@ template <class K> uint32_t shard_grid(K *kernel, uint64_t work, uint32_t dflt =
 template <bool VS, bool CL>
 void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
                   float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, void *recs,
-                  uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv, hipStream_t st) {
+                  uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv, hipStream_t st,
+                  uint32_t *tbin, uint32_t bin_cap) {
     const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
     hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
                        0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx,
-                       (RasterRec *)recs, live, clipq, ctr, counts, vrv);
+                       (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap);
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
     hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
-                       factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq, ctr, counts);
+                       factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq, ctr, counts, tbin, bin_cap);
 }
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
-                       uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag) {
+                       uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag, uint32_t *tbin,
+                       uint32_t bin_cap) {
     const uint64_t ns = tile_slots(W, rows_local);        // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
@@ -2915,14 +3005,18 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
             hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
                                cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr);
             setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
-                                      ctr, counts, nullptr, st);
+                                      ctr, counts, nullptr, st, tbin, bin_cap);
         } else if (vrv) {
             setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
-                                      ctr, counts, vrv, st);
+                                      ctr, counts, vrv, st, tbin, bin_cap);
         } else {
             setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live,
-                                       clipq, ctr, counts, nullptr, st);
+                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap);
         }
+    }
+    if (bin_cap) {                                       // bins mode: binned already
+        hipLaunchKernelGGL(k_tile_bins_done, dim3(1), dim3(64), 0, st, ctr, sum_host, tag);
+        return;
     }
     size_t bytes = scan_temp_bytes;
     (void)rocprim::exclusive_scan(scan_temp, bytes, (const uint32_t *)counts, offs, 0u, (size_t)ns,
@@ -2950,7 +3044,8 @@ void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, 
 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
-                        unsigned long long *keys, uint64_t cap, hipStream_t st, uint32_t ty0, uint32_t ty1) {
+                        unsigned long long *keys, uint64_t cap, hipStream_t st, uint32_t ty0, uint32_t ty1,
+                        uint32_t *counts, uint32_t bin_cap) {
     const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
     ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
     if (tx == 0 || ty0 >= ty1) return;
@@ -2958,7 +3053,7 @@ void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t np
     hipLaunchKernelGGL(k_tile_raster<false>, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
                        band, nparts, part, rows_local, tx, offs, ctr, list, keys,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx, none, (uint32_t *)nullptr, 0u,
-                       (uint4 *)nullptr);
+                       (uint4 *)nullptr, counts, bin_cap);
 }
 
 void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
@@ -2966,13 +3061,15 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
-                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows) {
+                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows, uint32_t *counts,
+                                uint32_t bin_cap) {
     const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
     hipLaunchKernelGGL(k_tile_raster<true>, dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band,
                        nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred);
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred,
+                       counts, bin_cap);
     hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred,
                        (const uint32_t *)ctr, out);
 }

@@ -78,7 +78,8 @@ constexpr uint64_t kLptMinBins = 2000;      // longest-first fragment order from
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
 // the order-independent tile path takes over (the icosahedron stress scene).
 constexpr uint64_t kRowPathMaxSlots = 8192;
-constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
+constexpr uint32_t kDefaultBand = 16;
+constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set       // rows per interleaved band when updateAndRender spans devices
 constexpr int kMaxDevices = 64;
 
 // S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
@@ -141,6 +142,11 @@ struct Dev {
     size_t keys_cap = 0;
     uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
     size_t deferred_cap = 0;
+    // bins mode (S3R_TILE_BINS): per buffer set, bin_cap entries for every (tile, bucket) slot
+    uint32_t *tbin[kSets] = {};
+    uint64_t tbin_slots[kSets] = {};           // slots each set's bins were allocated for
+    uint32_t bin_cap = 0;                      // entries per slot (grown when a frame overflows)
+    uint64_t bin_regrows = 0;                  // frames binned again into larger bins
     // host-coherent, per buffer set: {tag, live entries, list length, cluster-kept positions}, written
     // by k_tile_cursor as soon as they are known (tag = the frame's number)
     uint32_t *tile_sum_host = nullptr, *tile_sum_dev = nullptr;
@@ -336,6 +342,7 @@ struct Lib {
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
+    bool tile_bins = false;                    // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
     int tile_fused = -1;                       // tile path: raster and resolve in one launch (S3R_TILE_FUSED:
                                                // -1 whole frames only, the default; 0 never; 1 always)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
@@ -631,6 +638,8 @@ void initialize() {
         g.tile_slabs = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
         const char *l = getenv("S3R_TILE_LINE");
         g.tile_line_grid = !(l && atoi(l) == 0);
+        const char *tb = getenv("S3R_TILE_BINS");
+        g.tile_bins = tb && atoi(tb) != 0;
         const char *f = getenv("S3R_TILE_FUSED");
         g.tile_fused = f ? (atoi(f) != 0 ? 1 : 0) : -1;
     }
@@ -674,7 +683,7 @@ void dev_release(Dev &d) {
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases tile_ctr
         void *set[] = {d.tris[q], d.rowtab[q], d.bincnt[q], d.pairs[q], d.order[q], d.tile_counts[q], d.tile_offs[q],
-                       d.tile_cursor[q], d.tile_list[q], d.recs[q], d.live[q], d.tile_ctr[q]};
+                       d.tile_cursor[q], d.tile_list[q], d.recs[q], d.live[q], d.tile_ctr[q], d.tbin[q]};
         for (void *p : set)
             if (p) (void)hipFree(p);
     }
@@ -783,7 +792,7 @@ void restart_tags(Dev &d, uint32_t next_frame_no) {
         if (d.bincnt[p]) HIPCHECK(hipMemset(d.bincnt[p], 0, d.bins_cap * sizeof(uint32_t)));
     HIPCHECK(hipDeviceSynchronize());
     d.frame_no = next_frame_no;
-    if (d.tile_sum_host) memset(d.tile_sum_host, 0, 4 * kSets * sizeof(uint32_t));   // (tags restart)
+    if (d.tile_sum_host) memset(d.tile_sum_host, 0, kSumWords * kSets * sizeof(uint32_t));   // (tags restart)
     for (uint32_t &t : d.issued_tag) t = 0;
     d.last_tag = 0;
     if (d.done_host) __atomic_store_n(d.done_host, 0u, __ATOMIC_RELEASE);
@@ -864,8 +873,13 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                          bool frame_rows) {
     const float sw = (float)W, sh = (float)d.tile_H;
     const TileClusters cl = tile_clusters(d, nparts);
-    launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p], d.tile_list[p],
-                     d.tile_list_cap[p], geo);
+    const bool bins = d.tbin[p] != nullptr && g.tile_bins;
+    if (!bins)
+        launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p],
+                         d.tile_list[p], d.tile_list_cap[p], geo);
+    const uint32_t *list = bins ? d.tbin[p] : d.tile_list[p];
+    uint32_t *bcounts = bins ? d.tile_counts[p] : nullptr;
+    const uint32_t bcap = bins ? d.bin_cap : 0u;
     HIPCHECK(hipEventRecord(d.geo_done[p], geo));
     follow_previous_frame(d, st);
     HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
@@ -892,10 +906,10 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     if (fused) {
         launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                    d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
-                                   d.tile_list[p], d.tile_list_cap[p], d.deferred, st, frame_rows);
+                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap);
     } else if (slabs == 1u) {
-        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], d.tile_list[p],
-                           d.keys, d.tile_list_cap[p], st);
+        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list, d.keys,
+                           d.tile_list_cap[p], st, 0, 0xFFFFFFFFu, bcounts, bcap);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
                             sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
                             g.tile_line_grid, d.deferred, d.tile_ctr[p]);
@@ -910,8 +924,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
         }
         for (uint32_t k = 0; k < slabs; k++) {
             const uint32_t ty0 = (uint32_t)((uint64_t)tyn * k / slabs), ty1 = (uint32_t)((uint64_t)tyn * (k + 1) / slabs);
-            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
-                               d.tile_list[p], d.keys, d.tile_list_cap[p], st, ty0, ty1);
+            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list,
+                               d.keys, d.tile_list_cap[p], st, ty0, ty1, bcounts, bcap);
             HIPCHECK(hipEventRecord(d.slab_done[k], st));
             HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
             launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
@@ -942,15 +956,83 @@ void grow_tile_list(Dev &d, uint32_t p, uint64_t total) {
 // After a synchronous tile-path frame (its stream drained): if its list overflowed the capacity the
 // set had from earlier frames, render its fragment stage again into a list of the right size and
 // return true (the caller redoes its delivery); the totals are in tile_sum_host by then.
+// Spin until buffer set p's summary (k_tile_cursor / k_tile_bins_done) carries this frame's tag: a
+// stream synchronisation's wake-up costs ~10-20 us a frame; after 2 ms fall back to synchronising,
+// which also surfaces a device fault.
+void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
+    volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 1; __atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no; k++) {
+        __builtin_ia32_pause();
+        if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            HIPCHECK(hipStreamSynchronize(geo));
+            if (__atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no) {
+                fprintf(stderr, "s3r: tile path: the frame's summary never arrived\n");
+                abort();
+            }
+        }
+    }
+    d.last_pairs = sum[2];
+    d.last_live = sum[1];
+    d.last_kept = sum[3];
+    d.tile_readbacks++;
+}
+
+// Bins mode: every buffer set's bins for nt (tile, bucket) slots of d.bin_cap entries each (the
+// first capacity S3R_TILE_BIN_CAP or 256; grow_bins doubles it at least when a frame overflows).
+void ensure_bins(Dev &d, uint64_t nt) {
+    if (!d.bin_cap) {
+        const char *e = getenv("S3R_TILE_BIN_CAP");
+        d.bin_cap = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 256u;
+    }
+    for (int q = 0; q < kSets; q++) {
+        if (d.tbin[q] && d.tbin_slots[q] >= nt) continue;
+        HIPCHECK(hipDeviceSynchronize());
+        if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
+        d.tbin[q] = dalloc<uint32_t>(nt * d.bin_cap);
+        d.tbin_slots[q] = nt;
+    }
+}
+
+void grow_bins(Dev &d, uint32_t need) {
+    uint32_t cap = d.bin_cap * 2u;
+    while (cap < need + need / 4u) cap *= 2u;
+    HIPCHECK(hipDeviceSynchronize());
+    for (int q = 0; q < kSets; q++) {
+        if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
+        d.tbin[q] = dalloc<uint32_t>(d.tbin_slots[q] * cap);
+    }
+    d.bin_cap = cap;
+    d.bin_regrows++;
+}
+
+void bins_setup(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+                uint32_t rows_local, hipStream_t geo);
+
 bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     if (!d.tile_pending) return false;
     d.tile_pending = false;
     const uint32_t p = d.tile_pending_set;
-    const volatile uint32_t *sum = d.tile_sum_host + 4 * p;
+    const volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     const uint64_t total = sum[2];
     d.last_pairs = total;
     d.last_live = sum[1];
     d.last_kept = sum[3];
+    if (g.tile_bins && d.tbin[p]) {
+        if (sum[4] == 0) return false;
+        // a (tile, bucket) outgrew its bin: bin the frame again into larger bins (its raster, which
+        // rendered nothing, reset the counts), then its fragment stage
+        d.tile_overflows++;
+        hipStream_t geo = d.geo[0];
+        do {
+            grow_bins(d, sum[4]);
+            bins_setup(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
+        } while (sum[4] != 0);
+        tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
+                            nullptr, d.tile_frame_rows);
+        HIPCHECK(hipStreamSynchronize(st));
+        return true;
+    }
     if (total <= d.tile_list_cap[p]) return false;
     d.tile_overflows++;
     grow_tile_list(d, p, total);
@@ -960,6 +1042,18 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
                         nullptr, d.tile_frame_rows);
     HIPCHECK(hipStreamSynchronize(st));
     return true;
+}
+
+// Bins mode: buffer set p's setup again (into the grown bins; the counts zero), waiting for its summary.
+void bins_setup(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+                uint32_t rows_local, hipStream_t geo) {
+    const TileClusters cl = tile_clusters(d, nparts);
+    __atomic_store_n(&d.tile_sum_host[kSumWords * p], 0u, __ATOMIC_RELEASE);   // (the earlier pass carried this tag)
+    launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, (float)W, (float)H, W, band, nparts, part, rows_local,
+                      d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
+                      d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
+                      d.tbin[p], d.bin_cap);
+    wait_tile_summary(d, p, geo);
 }
 
 void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
@@ -1015,9 +1109,9 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
             HIPCHECK(hipMemset(d.tile_ctr[p], 0, kTileCtrWords * sizeof(uint32_t)));
             d.tile_total[p] = d.tile_ctr[p] + 1;
         }
-        HIPCHECK(hipHostMalloc((void **)&d.tile_sum_host, 4 * kSets * sizeof(uint32_t),
+        HIPCHECK(hipHostMalloc((void **)&d.tile_sum_host, kSumWords * kSets * sizeof(uint32_t),
                                hipHostMallocCoherent | hipHostMallocMapped));
-        memset(d.tile_sum_host, 0, 4 * kSets * sizeof(uint32_t));
+        memset(d.tile_sum_host, 0, kSumWords * kSets * sizeof(uint32_t));
         HIPCHECK(hipHostGetDevicePointer((void **)&d.tile_sum_dev, d.tile_sum_host, 0));
         HIPCHECK(hipDeviceSynchronize());          // (the null-stream memsets vs the geometry streams)
     }
@@ -1027,36 +1121,34 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (g.serial) wait_all_fragments(d, geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     const TileClusters cl = tile_clusters(d, nparts);
+    if (g.tile_bins) ensure_bins(d, nt);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
-                      d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + 4 * p, d.frame_no);
+                      d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
+                      g.tile_bins ? d.tbin[p] : nullptr, g.tile_bins ? d.bin_cap : 0u);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are
     // rendered again after the frame if it overflowed (tile_redo_if_overflowed; the fill and raster
     // kernels bound their list accesses).  S3R_TILE_READBACK=1: always read back.
     const bool readback_env = getenv("S3R_TILE_READBACK") && atoi(getenv("S3R_TILE_READBACK")) != 0;
-    volatile uint32_t *sum = d.tile_sum_host + 4 * p;
+    volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     d.last_path = 2;
     d.tile_H = H;
-    if (!sync || d.tile_list_cap[p] == 0 || readback_env) {
-        // spin on the summary k_tile_cursor publishes (a stream synchronisation's wake-up costs ~10-20
-        // us a frame); after 2 ms fall back to synchronising, which also surfaces a device fault
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t k = 1; __atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no; k++) {
-            __builtin_ia32_pause();
-            if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-                HIPCHECK(hipStreamSynchronize(geo));
-                if (__atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no) {
-                    fprintf(stderr, "s3r: tile path: the frame's summary never arrived\n");
-                    abort();
-                }
+    if (g.tile_bins) {
+        // bins mode: asynchronous frames check the bins before their fragment stage (a spin on the
+        // summary); synchronous ones after the frame (tile_redo_if_overflowed)
+        if (!sync || readback_env) {
+            wait_tile_summary(d, p, geo);
+            while (sum[4] != 0) {
+                d.tile_overflows++;
+                grow_bins(d, sum[4]);
+                HIPCHECK(hipMemsetAsync(d.tile_counts[p], 0, nt * sizeof(uint32_t), geo));   // the overflowed pass's
+                bins_setup(d, p, W, H, band, nparts, part, rows_local, geo);
             }
         }
-        d.last_pairs = sum[2];
-        d.last_live = sum[1];
-        d.last_kept = sum[3];
-        d.tile_readbacks++;
+    } else if (!sync || d.tile_list_cap[p] == 0 || readback_env) {
+        wait_tile_summary(d, p, geo);
         grow_tile_list(d, p, sum[2]);
     }
     tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts, frame_rows);
@@ -2300,6 +2392,12 @@ __attribute__((visibility("default"))) void s3r_tile_stats(uint64_t out[4]) {
     out[1] = d ? d->tile_overflows : 0;      // synchronous frames rendered again into a larger list
     out[2] = d ? d->last_pairs : 0;
     out[3] = d ? d->last_live : 0;           // live slots (meeting this part's rows), last read-back frame
+}
+
+__attribute__((visibility("default"))) float s3r_ooz_bound(const float ws[3], const float dx[3], const float dy[3],
+                                                           const float rvz[3], uint32_t xmin, uint32_t xmax,
+                                                           uint32_t ymin, uint32_t ymax) {
+    return ooz_bound_host(ws, dx, dy, rvz, xmin, xmax, ymin, ymax);
 }
 
 __attribute__((visibility("default"))) void s3r_cluster_stats(uint64_t out[4]) {

@@ -129,7 +129,11 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st,
                        float4 *vrv = nullptr, uint32_t nv = 0, const TileClusters *cl = nullptr,
-                       uint32_t *sum_host = nullptr, uint32_t tag = 0);
+                       uint32_t *sum_host = nullptr, uint32_t tag = 0, uint32_t *tbin = nullptr, uint32_t bin_cap = 0);
+// tbin / bin_cap (bins mode): every (tile, bucket) slot s gets bin_cap entries at tbin + s x bin_cap
+// and counts[s] of them filled by the setup itself -- no scan, no fill pass; the summary's word 4 is
+// then the count the fullest slot needed when it exceeded bin_cap (0: none; the frame is rendered
+// empty and must be binned again with larger bins), and offs / cursor / live are unused.
 // list: cap entries -- a frame whose list (ctr[1] entries) needs more writes only cap of them, and
 // k_tile_raster then renders no triangle (the caller renders the frame again with a larger list).
 // The fill's scatter cursors reset to the offsets (as launch_tile_setup leaves them): a frame's fill
@@ -146,7 +150,8 @@ void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                         unsigned long long *keys, uint64_t cap, hipStream_t st,
-                        uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu);   // tile rows [ty0, ty1) only
+                        uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu,    // tile rows [ty0, ty1) only
+                        uint32_t *counts = nullptr, uint32_t bin_cap = 0);   // bins mode: list = tbin
 // Raster and resolve in one launch (each tile shades its winners from LDS and stores them into out:
 // its local rows, or with frame_rows the frame rows of a W x H frame), then the pixels whose winner
 // needs a full setup (ctr[3] of them, in `deferred`: W x rows_local entries) in a second, short one.
@@ -155,7 +160,8 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
-                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows);
+                                uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows,
+                                uint32_t *counts = nullptr, uint32_t bin_cap = 0);
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
@@ -175,6 +181,8 @@ void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const flo
 void launch_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_rows, uint32_t W, uint32_t H,
                                uint32_t band, uint32_t nparts, uint32_t *frame, hipStream_t st);
 
+float ooz_bound_host(const float ws[3], const float dx[3], const float dy[3], const float rvz[3], uint32_t xmin,
+                     uint32_t xmax, uint32_t ymin, uint32_t ymax);
 void stats_read(unsigned long long out[24], bool reset);
 uint32_t wg_times_read(unsigned long long *out, uint32_t max_wg);
 uint32_t geo_times_read(unsigned long long *out, uint32_t max_wg);

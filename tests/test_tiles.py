@@ -393,3 +393,38 @@ def test_fused_raster_resolve_matches_oracle(gpu_renderer, scene_dir, icosa_dir,
         assert np.array_equal(got, want), diff(got, want)
     finally:
         r.set_raster_path('auto')
+
+
+@pytest.mark.parametrize('bin_cap', ['256', '4'])
+@pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
+def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, devices):
+    """Bins mode (S3R_TILE_BINS=1): the setup writes each slot straight into fixed-capacity bins of
+    its (tile, bucket)s -- no scan, no fill pass.  A tiny first capacity (S3R_TILE_BIN_CAP=4) makes
+    frames overflow: synchronous frames (updateAndRender, one device and three parts) are binned
+    again after the frame, asynchronous ones (s3r_render_bands) before their fragment stage."""
+    import torch
+    from oracle.oracle import OracleRenderer
+    monkeypatch.setenv('S3R_TILE_BINS', '1')
+    monkeypatch.setenv('S3R_TILE_BIN_CAP', bin_cap)
+    r = gpu_renderer
+    r.configure_devices(devices)
+    path = icosa_dir[2000]
+    r.configure(path)
+    try:
+        o = OracleRenderer(path)
+        seq = [(640, 480, (0, 0, 0, 0, 0, 0))] + [(640, 480, (40.0, 0, 0, 0, 0.0, 0.0))] * 6 + \\
+              [(1280, 720, (0, 0, 0, 0, 25.0, -10.0))] * 2
+        for k, (w, h, inp) in enumerate(seq):
+            got = r.update_and_render(w, h, inp)
+            want = o.update_and_render(w, h, inp)
+            assert np.array_equal(got, want), f'frame {k} {w}x{h}: ' + diff(got, want)
+        if bin_cap == '4':
+            assert r.tile_stats()['overflows'] > 0
+        if devices == [0]:
+            hold = (0, 0, 0, 0, 25.0, -10.0)
+            buf = torch.empty((720, 1280), dtype=torch.int32, device='cuda')
+            r.render_bands(hold, 1280, 720, 720, 1, 0, buf.data_ptr(), 0)
+            torch.cuda.synchronize()
+            assert np.array_equal(buf.cpu().numpy().view(np.uint32), want)
+    finally:
+        r.configure_devices([])
