@@ -29,6 +29,7 @@ import ctypes
 import json
 import os
 import platform
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -62,6 +63,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=10.0, help='CPU-baseline sample budget')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-device', action='store_true', help='skip the device-resident (HBM) rate')
+    p.add_argument('--data', default=None,
+                   help='data.bin path to reuse across runs (the deterministic scene is written there when missing)')
     return p.parse_args()
 
 
@@ -201,9 +204,16 @@ def run_rank0(a, N, np, torch):
     devices = [int(x) for x in a.devices.split(',')] if a.devices else list(range(N))
     if not a.devices and ndev < N:
         raise SystemExit(f'--gpus {N}: only {ndev} GPUs visible (use --devices to rehearse parts on one GPU)')
-    tmp = tempfile.mkdtemp(prefix='s3r_bench_')
-    data_path = os.path.join(tmp, f'{a.scene}.bin')
-    scene.write_named(a.scene, data_path)
+    tmp = None
+    if a.data and os.path.exists(a.data):
+        data_path = a.data
+    elif a.data:
+        data_path = a.data
+        scene.write_named(a.scene, data_path)
+    else:
+        tmp = tempfile.mkdtemp(prefix='s3r_bench_')
+        data_path = os.path.join(tmp, f'{a.scene}.bin')
+        scene.write_named(a.scene, data_path)
     W, H, B = a.width, a.height, a.band
     script = poses.script(a.pose)
     hold = poses.hold(a.pose)
@@ -340,6 +350,8 @@ def run_rank0(a, N, np, torch):
                          f'oracle/render_oracle.c (gcc -O2) on {cpu_model()}'}
     r.shutdown()
     buf.free()
+    if tmp:
+        shutil.rmtree(tmp, ignore_errors=True)
 
     frame_bytes = 4 * W * H
     return {

@@ -412,7 +412,7 @@ def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, d
     r.configure(path)
     try:
         o = OracleRenderer(path)
-        seq = [(640, 480, (0, 0, 0, 0, 0, 0))] + [(640, 480, (40.0, 0, 0, 0, 0.0, 0.0))] * 6 + \\
+        seq = [(640, 480, (0, 0, 0, 0, 0, 0))] + [(640, 480, (40.0, 0, 0, 0, 0.0, 0.0))] * 6 + \
               [(1280, 720, (0, 0, 0, 0, 25.0, -10.0))] * 2
         for k, (w, h, inp) in enumerate(seq):
             got = r.update_and_render(w, h, inp)

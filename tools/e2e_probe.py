@@ -59,6 +59,7 @@ def main():
     p.add_argument('--devices', default='0')
     p.add_argument('--torch', action='store_true', help='import torch and make device 0 current first (as bench.py)')
     p.add_argument('--warmup', type=int, default=30)
+    p.add_argument('--data', default=None, help='a data.bin to reuse (written there once when missing)')
     a = p.parse_args()
     if a.torch:
         import torch
@@ -69,8 +70,9 @@ def main():
     from swift3drenderer_amd import poses, scene
     from swift3drenderer_amd.abi import Input
     from swift3drenderer_amd.renderer import Renderer
-    path = os.path.join(tempfile.mkdtemp(), 's.bin')
-    scene.write_named(a.scene, path)
+    path = a.data or os.path.join(tempfile.mkdtemp(), 's.bin')
+    if not (a.data and os.path.exists(path)):
+        scene.write_named(a.scene, path)
     devs = [int(x) for x in a.devices.split(',')]
     r = Renderer(path, device=devs[0])
     r.configure_devices(devs if len(devs) > 1 else [])
