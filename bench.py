@@ -137,7 +137,9 @@ def load_traffic(workload_key):
 class DoubleBuffer:
     """main.swift:117-118, :164: one malloc of 2 * bufferSize, halves used alternately."""
 
-    def __init__(self, w, h):
+    def __init__(self, w, h, line_offset=None):
+        """line_offset (probes only): the buffer placed that many bytes past a 64-B line boundary
+        instead of where malloc puts it (glibc: 16 B past one)."""
         import numpy as np
         from swift3drenderer_amd.abi import PixelData
         self.libc = ctypes.CDLL(None)
@@ -145,9 +147,10 @@ class DoubleBuffer:
         self.libc.malloc.argtypes = [ctypes.c_size_t]
         self.libc.free.argtypes = [ctypes.c_void_p]
         self.size = 4 * w * h
-        self.ptr = self.libc.malloc(2 * self.size)
-        if not self.ptr:
+        self.raw = self.libc.malloc(2 * self.size + (128 if line_offset is not None else 0))
+        if not self.raw:
             raise MemoryError('malloc of the double buffer failed')
+        self.ptr = self.raw if line_offset is None else ((self.raw + 63) & ~63) + line_offset
         self.halves = [PixelData(ctypes.cast(self.ptr + k * self.size, ctypes.POINTER(ctypes.c_uint32)), w, h, 4,
                                  self.size) for k in (0, 1)]
         self.cur = 0
@@ -162,7 +165,7 @@ class DoubleBuffer:
         return (ctypes.c_uint8 * self.size).from_address(self.ptr + k * self.size)
 
     def free(self):
-        self.libc.free(self.ptr)
+        self.libc.free(self.raw)
 
 
 def main():

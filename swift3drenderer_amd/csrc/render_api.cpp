@@ -142,17 +142,18 @@ struct Dev {
     size_t keys_cap = 0;
     uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
     size_t deferred_cap = 0;
-    // bins mode (S3R_TILE_BINS): per buffer set, bin_cap entries for every (tile, bucket) slot
+    // bins (the default; S3R_TILE_BINS=0: the lists): per buffer set, bin_cap entries for every (tile, bucket) slot
     uint32_t *tbin[kSets] = {};
     uint64_t tbin_slots[kSets] = {};           // slots each set's bins were allocated for
     uint32_t bin_cap = 0;                      // entries per slot (grown when a frame overflows)
     uint64_t bin_regrows = 0;                  // frames binned again into larger bins
+    bool bins_off = false;                     // bins past the memory budget: this device uses the lists
     // host-coherent, per buffer set: {tag, live entries, list length, cluster-kept positions}, written
     // by k_tile_cursor as soon as they are known (tag = the frame's number)
     uint32_t *tile_sum_host = nullptr, *tile_sum_dev = nullptr;
     // a synchronous tile-path frame awaiting its overflow check (tile_redo_if_overflowed): its set
     // and what its fragment stage needs to run again
-    bool tile_pending = false;
+    bool tile_pending = false, tile_pending_bins = false;
     uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
     uint32_t *tile_out = nullptr;
     bool tile_frame_rows = false;
@@ -342,7 +343,8 @@ struct Lib {
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
     uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
-    bool tile_bins = false;                    // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
+    bool tile_bins = true;                     // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
+    uint64_t tile_bin_budget = 32ull << 30;    // bytes of bins per device, all buffer sets (S3R_TILE_BIN_BUDGET_MB)
     int tile_fused = -1;                       // tile path: raster and resolve in one launch (S3R_TILE_FUSED:
                                                // -1 whole frames only, the default; 0 never; 1 always)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
@@ -639,7 +641,9 @@ void initialize() {
         const char *l = getenv("S3R_TILE_LINE");
         g.tile_line_grid = !(l && atoi(l) == 0);
         const char *tb = getenv("S3R_TILE_BINS");
-        g.tile_bins = tb && atoi(tb) != 0;
+        g.tile_bins = !(tb && atoi(tb) == 0);
+        const char *bb = getenv("S3R_TILE_BIN_BUDGET_MB");
+        if (bb && atoll(bb) > 0) g.tile_bin_budget = (uint64_t)atoll(bb) << 20;
         const char *f = getenv("S3R_TILE_FUSED");
         g.tile_fused = f ? (atoi(f) != 0 ? 1 : 0) : -1;
     }
@@ -864,6 +868,8 @@ TileClusters tile_clusters(const Dev &d, uint32_t nparts) {
     return TileClusters{d.cl_sphere, d.cl_first, d.cl_perm, d.cl_shard, on ? g.ncl : 0u, d.cl_map};
 }
 
+bool bins_on(const Dev &d);
+
 // The tile path's fill and fragment stage of buffer set p (its setup done): scatter into the set's
 // list (capacity d.tile_list_cap[p]), raster, resolve into out, on st after the geometry stream.
 // frame_rows: out is the whole W x H frame (the caller's mapped buffer; direct delivery), each local
@@ -873,7 +879,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                          bool frame_rows) {
     const float sw = (float)W, sh = (float)d.tile_H;
     const TileClusters cl = tile_clusters(d, nparts);
-    const bool bins = d.tbin[p] != nullptr && g.tile_bins;
+    const bool bins = d.tbin[p] != nullptr && bins_on(d);
     if (!bins)
         launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p],
                          d.tile_list[p], d.tile_list_cap[p], geo);
@@ -978,12 +984,31 @@ void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
     d.tile_readbacks++;
 }
 
-// Bins mode: every buffer set's bins for nt (tile, bucket) slots of d.bin_cap entries each (the
-// first capacity S3R_TILE_BIN_CAP or 256; grow_bins doubles it at least when a frame overflows).
+// Bins mode (the default, S3R_TILE_BINS=0: the lists): every buffer set's bins for nt (tile, bucket)
+// slots of d.bin_cap entries each (the first capacity S3R_TILE_BIN_CAP or 256; grow_bins doubles it
+// at least when a frame overflows).  Bins are sized by the fullest (tile, bucket), so a scene piling
+// many triangles into one tile could need far more memory than its lists: past the budget
+// (S3R_TILE_BIN_BUDGET_MB, 32 GiB for all buffer sets) the device drops its bins and uses the lists.
+bool bins_on(const Dev &d) { return g.tile_bins && !d.bins_off; }
+
+void drop_bins(Dev &d) {
+    HIPCHECK(hipDeviceSynchronize());
+    for (int q = 0; q < kSets; q++) {
+        if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
+        d.tbin[q] = nullptr;
+        d.tbin_slots[q] = 0;
+    }
+    d.bins_off = true;
+}
+
 void ensure_bins(Dev &d, uint64_t nt) {
     if (!d.bin_cap) {
         const char *e = getenv("S3R_TILE_BIN_CAP");
         d.bin_cap = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 256u;
+    }
+    if ((uint64_t)kSets * nt * d.bin_cap * sizeof(uint32_t) > g.tile_bin_budget) {
+        drop_bins(d);
+        return;
     }
     for (int q = 0; q < kSets; q++) {
         if (d.tbin[q] && d.tbin_slots[q] >= nt) continue;
@@ -994,20 +1019,28 @@ void ensure_bins(Dev &d, uint64_t nt) {
     }
 }
 
-void grow_bins(Dev &d, uint32_t need) {
-    uint32_t cap = d.bin_cap * 2u;
-    while (cap < need + need / 4u) cap *= 2u;
+// Larger bins for a (tile, bucket) that needs `need` entries; false (bins dropped) past the budget.
+bool grow_bins(Dev &d, uint32_t need) {
+    uint64_t cap = (uint64_t)d.bin_cap * 2u;
+    while (cap < (uint64_t)need + need / 4u) cap *= 2u;
+    uint64_t total = 0;
+    for (int q = 0; q < kSets; q++) total += d.tbin_slots[q] * cap * sizeof(uint32_t);
+    if (total > g.tile_bin_budget || cap > 0x80000000ull) {
+        drop_bins(d);
+        return false;
+    }
     HIPCHECK(hipDeviceSynchronize());
     for (int q = 0; q < kSets; q++) {
         if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
         d.tbin[q] = dalloc<uint32_t>(d.tbin_slots[q] * cap);
     }
-    d.bin_cap = cap;
+    d.bin_cap = (uint32_t)cap;
     d.bin_regrows++;
+    return true;
 }
 
-void bins_setup(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                uint32_t rows_local, hipStream_t geo);
+void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+           uint32_t rows_local, hipStream_t geo);
 
 bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     if (!d.tile_pending) return false;
@@ -1018,16 +1051,13 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     d.last_pairs = total;
     d.last_live = sum[1];
     d.last_kept = sum[3];
-    if (g.tile_bins && d.tbin[p]) {
+    if (d.tile_pending_bins) {
         if (sum[4] == 0) return false;
-        // a (tile, bucket) outgrew its bin: bin the frame again into larger bins (its raster, which
-        // rendered nothing, reset the counts), then its fragment stage
+        // a (tile, bucket) outgrew its bin: bin the frame again into larger bins (or, past the budget,
+        // into the lists), then its fragment stage
         d.tile_overflows++;
         hipStream_t geo = d.geo[0];
-        do {
-            grow_bins(d, sum[4]);
-            bins_setup(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
-        } while (sum[4] != 0);
+        rebin(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
         tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
                             nullptr, d.tile_frame_rows);
         HIPCHECK(hipStreamSynchronize(st));
@@ -1044,16 +1074,29 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     return true;
 }
 
-// Bins mode: buffer set p's setup again (into the grown bins; the counts zero), waiting for its summary.
-void bins_setup(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
-                uint32_t rows_local, hipStream_t geo) {
+// Buffer set p's frame binned again after its bins overflowed (the summary's need in sum[4]), until it
+// fits: the counts zeroed (the overflowed pass left them counted -- k_tile_raster resets them only
+// where a raster ran), larger bins, the setup again, waiting for its summary; past the budget the set
+// is set up into the lists instead (grow_bins dropped the bins, so its fragment stage reads the lists).
+void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
+           uint32_t rows_local, hipStream_t geo) {
     const TileClusters cl = tile_clusters(d, nparts);
-    __atomic_store_n(&d.tile_sum_host[kSumWords * p], 0u, __ATOMIC_RELEASE);   // (the earlier pass carried this tag)
-    launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, (float)W, (float)H, W, band, nparts, part, rows_local,
-                      d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p],
-                      d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      d.tbin[p], d.bin_cap);
-    wait_tile_summary(d, p, geo);
+    volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
+    const uint64_t nt = tile_slots(W, rows_local);
+    while (sum[4] != 0) {
+        const bool bins = grow_bins(d, sum[4]);
+        HIPCHECK(hipMemsetAsync(d.tile_counts[p], 0, nt * sizeof(uint32_t), geo));
+        __atomic_store_n(&d.tile_sum_host[kSumWords * p], 0u, __ATOMIC_RELEASE);   // (the earlier pass carried this tag)
+        launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, (float)W, (float)H, W, band, nparts, part, rows_local,
+                          d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p],
+                          d.tile_cursor[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl,
+                          d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u);
+        wait_tile_summary(d, p, geo);
+        if (!bins) {
+            grow_tile_list(d, p, sum[2]);
+            break;
+        }
+    }
 }
 
 void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
@@ -1121,11 +1164,12 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (g.serial) wait_all_fragments(d, geo);
     if (ts) HIPCHECK(hipEventRecord(ts->frame0, geo));
     const TileClusters cl = tile_clusters(d, nparts);
-    if (g.tile_bins) ensure_bins(d, nt);
+    if (bins_on(d)) ensure_bins(d, nt);
+    const bool bins = bins_on(d);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      g.tile_bins ? d.tbin[p] : nullptr, g.tile_bins ? d.bin_cap : 0u);
+                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are
@@ -1135,16 +1179,14 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     d.last_path = 2;
     d.tile_H = H;
-    if (g.tile_bins) {
+    if (bins) {
         // bins mode: asynchronous frames check the bins before their fragment stage (a spin on the
         // summary); synchronous ones after the frame (tile_redo_if_overflowed)
         if (!sync || readback_env) {
             wait_tile_summary(d, p, geo);
-            while (sum[4] != 0) {
+            if (sum[4] != 0) {
                 d.tile_overflows++;
-                grow_bins(d, sum[4]);
-                HIPCHECK(hipMemsetAsync(d.tile_counts[p], 0, nt * sizeof(uint32_t), geo));   // the overflowed pass's
-                bins_setup(d, p, W, H, band, nparts, part, rows_local, geo);
+                rebin(d, p, W, H, band, nparts, part, rows_local, geo);
             }
         }
     } else if (!sync || d.tile_list_cap[p] == 0 || readback_env) {
@@ -1155,6 +1197,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (sync) {
         // the overflow check reads this frame's summary once the frame is done
         d.tile_pending = true;
+        d.tile_pending_bins = bins && bins_on(d);
         d.tile_pending_set = p;
         d.tile_W = W; d.tile_band = band; d.tile_nparts = nparts; d.tile_part = part; d.tile_rows = rows_local;
         d.tile_out = out;

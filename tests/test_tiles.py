@@ -267,8 +267,10 @@ def test_sync_frames_without_list_readback(gpu_renderer, icosa_dir, monkeypatch)
     """updateAndRender frames on the tile path size each buffer set's list from earlier frames (no
     host sync before the fill); a frame whose list overflowed is rendered again into a larger one.
     With no headroom (S3R_TILE_LIST_EXACT=1) walking towards the icosahedra grows the list every
-    few frames: every frame must still equal the oracle's, and some must have been redone."""
+    few frames: every frame must still equal the oracle's, and some must have been redone.  (The lists:
+    S3R_TILE_BINS=0; bins overflow in test_tile_bins_match_oracle.)"""
     from oracle.oracle import OracleRenderer
+    monkeypatch.setenv('S3R_TILE_BINS', '0')
     monkeypatch.setenv('S3R_TILE_LIST_EXACT', '1')
     path = icosa_dir[2000]
     r = gpu_renderer
@@ -289,15 +291,21 @@ def test_sync_frames_without_list_readback(gpu_renderer, icosa_dir, monkeypatch)
         r.set_raster_path('auto')
 
 
+@pytest.mark.parametrize('store', ['bins', 'lists'])
 @pytest.mark.parametrize('mode', ['copy', 'direct', 'auto'])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
-def test_tile_deliveries_match_oracle(gpu_renderer, icosa_dir, monkeypatch, mode, devices):
+def test_tile_deliveries_match_oracle(gpu_renderer, icosa_dir, monkeypatch, mode, devices, store):
     """Tile-path frames (the stress scene) delivered by copy, or written by the resolve kernel straight
     into their rows of the caller's buffer (direct; 'auto' picks it, host fill being a row-path
     delivery) -- on one device and three parts, into the halves of a double buffer, with frames whose
-    list overflowed (S3R_TILE_LIST_EXACT=1) rendered again into the same rows."""
+    list overflowed (S3R_TILE_LIST_EXACT=1) or whose bins overflowed (S3R_TILE_BIN_CAP=4) rendered
+    again into the same rows."""
     from oracle.oracle import OracleRenderer
-    monkeypatch.setenv('S3R_TILE_LIST_EXACT', '1')
+    if store == 'lists':
+        monkeypatch.setenv('S3R_TILE_BINS', '0')
+        monkeypatch.setenv('S3R_TILE_LIST_EXACT', '1')
+    else:
+        monkeypatch.setenv('S3R_TILE_BIN_CAP', '4')
     r = gpu_renderer
     r.configure_devices(devices)
     path = icosa_dir[2000]
@@ -395,17 +403,22 @@ def test_fused_raster_resolve_matches_oracle(gpu_renderer, scene_dir, icosa_dir,
         r.set_raster_path('auto')
 
 
-@pytest.mark.parametrize('bin_cap', ['256', '4'])
+@pytest.mark.parametrize('bin_cap,budget_mb', [('256', ''), ('4', ''), ('4', '1'), ('256', '1')])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
-def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, devices):
-    """Bins mode (S3R_TILE_BINS=1): the setup writes each slot straight into fixed-capacity bins of
-    its (tile, bucket)s -- no scan, no fill pass.  A tiny first capacity (S3R_TILE_BIN_CAP=4) makes
+def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, budget_mb, devices):
+    """Bins mode (the default): the setup writes each slot straight into fixed-capacity bins of its
+    (tile, bucket)s -- no scan, no fill pass.  A tiny first capacity (S3R_TILE_BIN_CAP=4) makes
     frames overflow: synchronous frames (updateAndRender, one device and three parts) are binned
-    again after the frame, asynchronous ones (s3r_render_bands) before their fragment stage."""
+    again after the frame, asynchronous ones (s3r_render_bands) before their fragment stage.  With a
+    1-MiB budget (S3R_TILE_BIN_BUDGET_MB) the grown bins (cap 4) or the first ones (cap 256: 640x480
+    is 9 600 (tile, bucket)s, 9.8 MB for four buffer sets) do not fit: the device falls back to the
+    lists, mid-frame or from the start."""
     import torch
     from oracle.oracle import OracleRenderer
     monkeypatch.setenv('S3R_TILE_BINS', '1')
     monkeypatch.setenv('S3R_TILE_BIN_CAP', bin_cap)
+    if budget_mb:
+        monkeypatch.setenv('S3R_TILE_BIN_BUDGET_MB', budget_mb)
     r = gpu_renderer
     r.configure_devices(devices)
     path = icosa_dir[2000]

@@ -59,6 +59,7 @@ def main():
     p.add_argument('--devices', default='0')
     p.add_argument('--torch', action='store_true', help='import torch and make device 0 current first (as bench.py)')
     p.add_argument('--warmup', type=int, default=30)
+    p.add_argument('--line-offset', type=int, default=None, help='buffer this many bytes past a 64-B line')
     p.add_argument('--data', default=None, help='a data.bin to reuse (written there once when missing)')
     a = p.parse_args()
     if a.torch:
@@ -79,7 +80,7 @@ def main():
     r.configure(path, devs[0])
     r.set_delivery(a.delivery, a.fill_threads)
     W, H = a.width, a.height
-    buf = DoubleBuffer(W, H)
+    buf = DoubleBuffer(W, H, a.line_offset)
     for t in poses.script(a.pose):
         r.lib.updateAndRender(ctypes.byref(buf.next()), ctypes.byref(Input.of(t)))
     hold = Input.of(poses.hold(a.pose))
