@@ -1711,9 +1711,11 @@ __device__ __forceinline__ TileSpan box_tiles(uint32_t bt, uint32_t by, uint32_t
     sp.bucket = bt >> 24;
     return sp;
 }
-// The packed tile box of a raster record's pixel bbox bx = xmin | xmax << 16 and bound bits zb.
-__device__ __forceinline__ uint32_t tile_box(uint32_t bx, uint32_t zb) {
-    return ((bx & 0xFFFFu) / kTileW) | (((bx >> 16) / kTileW) << 12) | (depth_bucket(zb) << 24);
+// The packed tile box of a raster record's pixel bbox bx = xmin | xmax << 16 and bound bits zb, on a
+// tile grid shifted left by xoff pixels (tile column c covers x in [64 c - xoff, 64 c - xoff + 64);
+// k_tile_raster, tile_grid_x).
+__device__ __forceinline__ uint32_t tile_box(uint32_t bx, uint32_t zb, uint32_t xoff) {
+    return (((bx & 0xFFFFu) + xoff) / kTileW) | ((((bx >> 16) + xoff) / kTileW) << 12) | (depth_bucket(zb) << 24);
 }
 static_assert(kDepthBuckets <= 64, "bucket field of a packed tile box");
 
@@ -1950,7 +1952,7 @@ __device__ __forceinline__ void wave_append_u32(bool want, uint32_t v, uint32_t 
 // Bins mode (tbin non-null, kernels.hip "bins"): the slot goes straight into the fixed-capacity
 // bins of its (tile, bucket)s -- no live entry, no fill pass.
 __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_t slot, uint32_t band, uint32_t nparts,
-                                          uint32_t part, uint32_t tiles_x, RasterRec *__restrict__ recs,
+                                          uint32_t part, uint32_t tiles_x, uint32_t xoff, RasterRec *__restrict__ recs,
                                           uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
                                           uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin = nullptr,
                                           uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr) {
@@ -1958,7 +1960,7 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
         const uint32_t zb = f2u(ooz_bound(ts));
-        const uint32_t bt = tile_box(ts.xmin | (ts.xmax << 16), zb);
+        const uint32_t bt = tile_box(ts.xmin | (ts.xmax << 16), zb, xoff);
         sp = box_tiles(bt, ts.ymin | (ts.ymax << 16), band, nparts, part);
         if (sp.n) {
             bx = bt;
@@ -1967,6 +1969,9 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
         }
     }
     if (tbin) {
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 16)
+        if (bx == 12345u)                               // ablation: no binning
+#endif
         tile_visit(sp, tiles_x, counts, tbin, slot, 0xFFFFFFFFu, bin_cap, ovf);
         return;
     }
@@ -1992,7 +1997,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
                                                     const uint32_t *__restrict__ shard_tab,
                                                     Mat34 m, float factor, float sw, float sh,
                                                     uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
-                                                    RasterRec *__restrict__ recs, uint4 *__restrict__ live,
+                                                    uint32_t xoff, RasterRec *__restrict__ recs, uint4 *__restrict__ live,
                                                     uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
                                                     uint32_t *__restrict__ counts, const float4 *__restrict__ vrv,
                                                     uint32_t *__restrict__ tbin, uint32_t bin_cap) {
@@ -2047,7 +2052,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -2061,7 +2066,7 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
                                                    const uint32_t *__restrict__ shard_tab,
                                                    Mat34 m, float factor, float sw, float sh,
                                                    uint32_t band, uint32_t nparts, uint32_t part, uint32_t tiles_x,
-                                                   RasterRec *__restrict__ recs, uint4 *__restrict__ live,
+                                                   uint32_t xoff, RasterRec *__restrict__ recs, uint4 *__restrict__ live,
                                                    const uint32_t *__restrict__ clipq, uint32_t *__restrict__ ctr,
                                                    uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin,
                                                    uint32_t bin_cap) {
@@ -2095,8 +2100,8 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
             if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) live_a = raster_part(app, sw, sh, ta);
             live_t = raster_part(d, sw, sh, ts);
         }
-        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -2297,7 +2302,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
     const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0,
     ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred,
-    uint32_t *__restrict__ counts, uint32_t bin_cap) {
+    uint32_t *__restrict__ counts, uint32_t bin_cap, uint32_t xoff) {
     __shared__ TileShared ls;
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
@@ -2306,7 +2311,8 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         *shard_ctr(ctr, 1, threadIdx.x) = 0u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = tile0 + blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    const uint32_t lx0 = tx * kTileW, lx1 = min(W, lx0 + kTileW) - 1u;
+    // the tile's pixel columns: [64 tx - xoff, 64 tx - xoff + 64) inside the frame (tile_box)
+    const uint32_t lx0 = max(tx * kTileW, xoff) - xoff, lx1 = min(W, tx * kTileW + kTileW - xoff) - 1u;
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
     const float ib = udiv_inv(band);
     auto row_of = [&](uint32_t lr) {
@@ -2922,11 +2928,15 @@ float ooz_bound_host(const float ws[3], const float dx[3], const float dy[3], co
     return ooz_bound(t);
 }
 
-uint32_t tile_grid_x(uint32_t W) { return (W + kTileW - 1) / kTileW; }
+uint32_t tile_grid_x(uint32_t W, uint32_t xoff = 0) { return (W + xoff + kTileW - 1) / kTileW; }
 uint32_t tile_height() { return kTileH; }
 static_assert(kTileH % 4u == 0, "tile rows = whole 4-row resolve blocks (slabbed fragment stage)");
-uint32_t tile_count(uint32_t W, uint32_t rows_local) { return tile_grid_x(W) * ((rows_local + kTileH - 1) / kTileH); }
-uint64_t tile_slots(uint32_t W, uint32_t rows_local) { return (uint64_t)tile_count(W, rows_local) * kDepthBuckets; }
+uint32_t tile_count(uint32_t W, uint32_t rows_local, uint32_t xoff) {
+    return tile_grid_x(W, xoff) * ((rows_local + kTileH - 1) / kTileH);
+}
+uint64_t tile_slots(uint32_t W, uint32_t rows_local, uint32_t xoff) {
+    return (uint64_t)tile_count(W, rows_local, xoff) * kDepthBuckets;
+}
 
 size_t tile_scan_temp_bytes(uint64_t nslots) {
     size_t bytes = 0;
@@ -2977,16 +2987,17 @@ template <class K> uint32_t shard_grid(K *kernel, uint64_t work, uint32_t dflt =
 
 template <bool VS, bool CL>
 void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
-                  float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, void *recs,
-                  uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv, hipStream_t st,
-                  uint32_t *tbin, uint32_t bin_cap) {
+                  float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
+                  void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
+                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap) {
     const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
     hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
-                       0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx,
+                       0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, xoff,
                        (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap);
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
     hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
-                       factor, sw, sh, band, nparts, part, tx, (RasterRec *)recs, live, clipq, ctr, counts, tbin, bin_cap);
+                       factor, sw, sh, band, nparts, part, tx, xoff, (RasterRec *)recs, live, clipq, ctr, counts, tbin,
+                       bin_cap);
 }
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
@@ -2994,23 +3005,23 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
                        uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag, uint32_t *tbin,
-                       uint32_t bin_cap) {
-    const uint64_t ns = tile_slots(W, rows_local);        // (counts and ctr's shard counters: left zeroed)
+                       uint32_t bin_cap, uint32_t xoff) {
+    const uint64_t ns = tile_slots(W, rows_local, xoff);  // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
         hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv);
     if (ntri) {
-        const uint32_t tx = tile_grid_x(W);
+        const uint32_t tx = tile_grid_x(W, xoff);
         if (clustered) {
             hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
                                cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr);
-            setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
+            setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
                                       ctr, counts, nullptr, st, tbin, bin_cap);
         } else if (vrv) {
-            setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live, clipq,
+            setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
                                       ctr, counts, vrv, st, tbin, bin_cap);
         } else {
-            setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, recs, live,
+            setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live,
                                        clipq, ctr, counts, nullptr, st, tbin, bin_cap);
         }
     }
@@ -3026,8 +3037,8 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
 }
 
 void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
-                        uint32_t *ctr, hipStream_t st) {
-    const uint64_t ns = tile_slots(W, rows_local);
+                        uint32_t *ctr, hipStream_t st, uint32_t xoff) {
+    const uint64_t ns = tile_slots(W, rows_local, xoff);
     if (ns == 0) return;
     hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, (uint32_t *)counts, offs,
                        (uint32_t)ns, cursor, ctr, 0u, (uint32_t *)nullptr, 0u);
@@ -3035,25 +3046,25 @@ void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W
 
 void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
                       uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
-                      hipStream_t st) {
+                      hipStream_t st, uint32_t xoff) {
     if (ntri == 0) return;
     hipLaunchKernelGGL(k_tile_fill, dim3(shard_grid(k_tile_fill, ntri)), dim3(256), 0, st, live, ctr,
-                       cl && cl->ncl ? cl->shard : nullptr, ntri, band, nparts, part, tile_grid_x(W), cursor, list,
+                       cl && cl->ncl ? cl->shard : nullptr, ntri, band, nparts, part, tile_grid_x(W, xoff), cursor, list,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
 }
 
 void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                         uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                         unsigned long long *keys, uint64_t cap, hipStream_t st, uint32_t ty0, uint32_t ty1,
-                        uint32_t *counts, uint32_t bin_cap) {
-    const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
+                        uint32_t *counts, uint32_t bin_cap, uint32_t xoff) {
+    const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
     if (tx == 0 || ty0 >= ty1) return;
     const ShadeScene none{};
     hipLaunchKernelGGL(k_tile_raster<false>, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
                        band, nparts, part, rows_local, tx, offs, ctr, list, keys,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx, none, (uint32_t *)nullptr, 0u,
-                       (uint4 *)nullptr, counts, bin_cap);
+                       (uint4 *)nullptr, counts, bin_cap, xoff);
 }
 
 void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
@@ -3062,14 +3073,14 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows, uint32_t *counts,
-                                uint32_t bin_cap) {
-    const uint32_t tx = tile_grid_x(W), ty = (rows_local + kTileH - 1) / kTileH;
+                                uint32_t bin_cap, uint32_t xoff) {
+    const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
     hipLaunchKernelGGL(k_tile_raster<true>, dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band,
                        nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred,
-                       counts, bin_cap);
+                       counts, bin_cap, xoff);
     hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred,
                        (const uint32_t *)ctr, out);
 }

@@ -154,6 +154,7 @@ struct Dev {
     // a synchronous tile-path frame awaiting its overflow check (tile_redo_if_overflowed): its set
     // and what its fragment stage needs to run again
     bool tile_pending = false, tile_pending_bins = false;
+    uint32_t tile_xoff = 0;                    // the current frame's tile-grid shift (tile_xoff_for)
     uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
     uint32_t *tile_out = nullptr;
     bool tile_frame_rows = false;
@@ -882,7 +883,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     const bool bins = d.tbin[p] != nullptr && bins_on(d);
     if (!bins)
         launch_tile_fill(d.live[p], d.tile_ctr[p], &cl, g.ntri, W, band, nparts, part, d.tile_cursor[p],
-                         d.tile_list[p], d.tile_list_cap[p], geo);
+                         d.tile_list[p], d.tile_list_cap[p], geo, d.tile_xoff);
     const uint32_t *list = bins ? d.tbin[p] : d.tile_list[p];
     uint32_t *bcounts = bins ? d.tile_counts[p] : nullptr;
     const uint32_t bcap = bins ? d.bin_cap : 0u;
@@ -912,10 +913,10 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     if (fused) {
         launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                    d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
-                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap);
+                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff);
     } else if (slabs == 1u) {
         launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list, d.keys,
-                           d.tile_list_cap[p], st, 0, 0xFFFFFFFFu, bcounts, bcap);
+                           d.tile_list_cap[p], st, 0, 0xFFFFFFFFu, bcounts, bcap, d.tile_xoff);
         launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
                             sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
                             g.tile_line_grid, d.deferred, d.tile_ctr[p]);
@@ -931,7 +932,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
         for (uint32_t k = 0; k < slabs; k++) {
             const uint32_t ty0 = (uint32_t)((uint64_t)tyn * k / slabs), ty1 = (uint32_t)((uint64_t)tyn * (k + 1) / slabs);
             launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list,
-                               d.keys, d.tile_list_cap[p], st, ty0, ty1, bcounts, bcap);
+                               d.keys, d.tile_list_cap[p], st, ty0, ty1, bcounts, bcap, d.tile_xoff);
             HIPCHECK(hipEventRecord(d.slab_done[k], st));
             HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
             launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
@@ -1067,7 +1068,8 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
     d.tile_overflows++;
     grow_tile_list(d, p, total);
     hipStream_t geo = d.geo[0];
-    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_ctr[p], geo);
+    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_ctr[p], geo,
+                       d.tile_xoff);
     tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
                         nullptr, d.tile_frame_rows);
     HIPCHECK(hipStreamSynchronize(st));
@@ -1082,7 +1084,7 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
            uint32_t rows_local, hipStream_t geo) {
     const TileClusters cl = tile_clusters(d, nparts);
     volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
-    const uint64_t nt = tile_slots(W, rows_local);
+    const uint64_t nt = tile_slots(W, rows_local, d.tile_xoff);
     while (sum[4] != 0) {
         const bool bins = grow_bins(d, sum[4]);
         HIPCHECK(hipMemsetAsync(d.tile_counts[p], 0, nt * sizeof(uint32_t), geo));
@@ -1090,7 +1092,8 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
         launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, (float)W, (float)H, W, band, nparts, part, rows_local,
                           d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p],
                           d.tile_cursor[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl,
-                          d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u);
+                          d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u,
+                          d.tile_xoff);
         wait_tile_summary(d, p, geo);
         if (!bins) {
             grow_tile_list(d, p, sum[2]);
@@ -1106,7 +1109,13 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         exit(1);
     }
     const float sw = (float)W, sh = (float)H;
-    const uint64_t nt = tile_slots(W, rows_local);          // (tile, depth bucket) entries
+    // a frame written into the caller's buffer: tiles on its 64-B line grid -- a malloc'd buffer starts
+    // 16 B into a line, so 64-px tiles at x = 64 c would store each tile row as five lines, two partly
+    // written; shifted left by that offset (W a multiple of 16, so every row shares it) each tile row
+    // crosses the link as four whole lines (stress frame, one MI355X: 689-710 fps at the malloc offset,
+    // 741-747 into a line-aligned buffer, profiles/r04_line_offset.txt)
+    d.tile_xoff = frame_rows && g.tile_line_grid && W % 16u == 0u ? (uint32_t)(((uintptr_t)out >> 2) & 15u) : 0u;
+    const uint64_t nt = tile_slots(W, rows_local, d.tile_xoff);   // (tile, depth bucket) entries
     if (d.tiles_cap < nt) {
         HIPCHECK(hipDeviceSynchronize());
         for (int p = 0; p < kSets; p++) {
@@ -1169,7 +1178,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u);
+                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are

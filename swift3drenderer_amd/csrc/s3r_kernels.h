@@ -91,9 +91,12 @@ void fragment_configure(uint32_t W, uint32_t rows_local);
 // each tile's list split into depth buckets (nearest first; kernels.hip depth_bucket).
 // recs: 2T x raster_rec_bytes(); counts / offs / cursor: tile_slots() (tile, bucket) entries;
 // scan_temp: tile_scan_temp_bytes(tile_slots()) bytes.
-uint32_t tile_count(uint32_t W, uint32_t rows_local);
+// xoff (every tile launch of a frame the same): the tile grid shifted left by xoff < 16 pixels, tile
+// column c covering x in [64 c - xoff, 64 c - xoff + 64) -- a frame written into the caller's
+// buffer puts each tile row's 64 pixels on the buffer's 64-B line grid (render_api.cpp tile_xoff).
+uint32_t tile_count(uint32_t W, uint32_t rows_local, uint32_t xoff = 0);
 uint32_t tile_height();                        // rows of a tile (a multiple of the resolve's 4-row blocks)
-uint64_t tile_slots(uint32_t W, uint32_t rows_local);
+uint64_t tile_slots(uint32_t W, uint32_t rows_local, uint32_t xoff = 0);
 size_t tile_scan_temp_bytes(uint64_t nslots);
 size_t raster_rec_bytes();
 // Init-time clusters (clusters.cpp) on the device: ncl bounding spheres (world centre, radius),
@@ -129,7 +132,8 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st,
                        float4 *vrv = nullptr, uint32_t nv = 0, const TileClusters *cl = nullptr,
-                       uint32_t *sum_host = nullptr, uint32_t tag = 0, uint32_t *tbin = nullptr, uint32_t bin_cap = 0);
+                       uint32_t *sum_host = nullptr, uint32_t tag = 0, uint32_t *tbin = nullptr, uint32_t bin_cap = 0,
+                       uint32_t xoff = 0);
 // tbin / bin_cap (bins mode): every (tile, bucket) slot s gets bin_cap entries at tbin + s x bin_cap
 // and counts[s] of them filled by the setup itself -- no scan, no fill pass; the summary's word 4 is
 // then the count the fullest slot needed when it exceeded bin_cap (0: none; the frame is rendered
@@ -139,11 +143,11 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
 // The fill's scatter cursors reset to the offsets (as launch_tile_setup leaves them): a frame's fill
 // again, e.g. into a larger list after an overflow.
 void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
-                        uint32_t *ctr, hipStream_t st);
+                        uint32_t *ctr, hipStream_t st, uint32_t xoff = 0);
 // The same cl as the setup's (it says where the shards' live entries start).
 void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
                       uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
-                      hipStream_t st);
+                      hipStream_t st, uint32_t xoff = 0);
 // keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
 // ctr: the setup's counters (its list length ctr[1]; the launch of tile row 0 resets the live counters
 // when the list did not overflow).
@@ -151,7 +155,8 @@ void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t np
                         uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                         unsigned long long *keys, uint64_t cap, hipStream_t st,
                         uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu,    // tile rows [ty0, ty1) only
-                        uint32_t *counts = nullptr, uint32_t bin_cap = 0);   // bins mode: list = tbin
+                        uint32_t *counts = nullptr, uint32_t bin_cap = 0,    // bins mode: list = tbin
+                        uint32_t xoff = 0);
 // Raster and resolve in one launch (each tile shades its winners from LDS and stores them into out:
 // its local rows, or with frame_rows the frame rows of a W x H frame), then the pixels whose winner
 // needs a full setup (ctr[3] of them, in `deferred`: W x rows_local entries) in a second, short one.
@@ -161,7 +166,7 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows,
-                                uint32_t *counts = nullptr, uint32_t bin_cap = 0);
+                                uint32_t *counts = nullptr, uint32_t bin_cap = 0, uint32_t xoff = 0);
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,

@@ -403,7 +403,39 @@ def test_fused_raster_resolve_matches_oracle(gpu_renderer, scene_dir, icosa_dir,
         r.set_raster_path('auto')
 
 
-@pytest.mark.parametrize('bin_cap,budget_mb', [('256', ''), ('4', ''), ('4', '1'), ('256', '1')])
+@pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
+def test_tile_line_offsets_match_oracle(gpu_renderer, icosa_dir, devices):
+    """Direct delivery puts the tile grid on the caller buffer's 64-B line grid (render_api.cpp
+    render_tiles: tile column c covers x in [64 c - xoff, 64 c - xoff + 64), xoff = the buffer's pixel
+    offset into its line): buffers starting 0, 4, 16, 36 and 60 B past a line, and a width that is not a
+    multiple of 16 (no shift), all give the oracle's pixels."""
+    from oracle.oracle import OracleRenderer
+    r = gpu_renderer
+    r.configure_devices(devices)
+    path = icosa_dir[2000]
+    r.configure(path)
+    r.set_delivery('direct')
+    try:
+        o = OracleRenderer(path)
+        inp = (40.0, 0, 0, 0, 25.0, -10.0)
+        keep = []                               # (registered by the library: alive until the end)
+        for w, h, offs in [(640, 480, (0, 4, 16, 36, 60)), (1000, 360, (16,))]:
+            for off in offs:
+                want = o.update_and_render(w, h, inp)       # (both cameras move on each frame)
+                mem = np.empty(w * h + 16, dtype=np.uint32)
+                keep.append(mem)
+                i = next(k for k in range(16) if (mem.ctypes.data + 4 * k) % 64 == off)
+                half = mem[i:i + w * h].reshape(h, w)
+                half[:] = 0x5A5A5A5A
+                got = r.update_and_render(w, h, inp, half)
+                assert np.array_equal(got, want), f'{w}x{h} at +{off} B: ' + diff(got, want)
+        assert r.raster_path() == 'tiles'
+    finally:
+        r.set_delivery('env')
+        r.configure_devices([])
+
+
+@pytest.mark.parametrize('bin_cap,budget_mb',[('256', ''), ('4', ''), ('4', '1'), ('256', '1')])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
 def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, budget_mb, devices):
     """Bins mode (the default): the setup writes each slot straight into fixed-capacity bins of its
