@@ -1732,7 +1732,14 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t rounds = sp.n;
     for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
-    constexpr uint32_t kSteps = 4;                       // steps whose atomics are in flight together
+#ifndef S3R_TV_STEPS
+#define S3R_TV_STEPS 2
+#endif
+    // steps whose atomics are in flight together: a wave's lanes rarely span more than 1-2 tiles, so
+    // wider steps mostly run empty ballot rounds (stress scene, bins: 4 -> 2 steps, whole-frame setup
+    // 620-627 -> 595 us, part 0 of 8 148 -> 128 us; 8 steps 657, 1 step 606 / 131;
+    // profiles/r04_setup_ab.txt)
+    constexpr uint32_t kSteps = S3R_TV_STEPS;
     for (uint32_t k0 = 0; k0 < rounds; k0 += kSteps) {
         uint32_t key[kSteps], leader_of[kSteps], rank[kSteps], base[kSteps];
 #pragma unroll

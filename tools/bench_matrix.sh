@@ -19,4 +19,4 @@ run --scene full --pose P_over
 run --scene full --pose P_id
 run --scene full --pose P_clip
 run --scene full --pose P_over --width 7680 --height 4320
-run --scene icosa-stress --pose P_id --steps 50 --warmup 5
+run --scene icosa-stress --pose P_id --steps 50 --warmup 5 --data /tmp/s3r_stress.bin
