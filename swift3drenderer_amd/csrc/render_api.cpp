@@ -346,8 +346,7 @@ struct Lib {
     bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
     bool tile_bins = true;                     // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
     uint64_t tile_bin_budget = 32ull << 30;    // bytes of bins per device, all buffer sets (S3R_TILE_BIN_BUDGET_MB)
-    int tile_fused = -1;                       // tile path: raster and resolve in one launch (S3R_TILE_FUSED:
-                                               // -1 whole frames only, the default; 0 never; 1 always)
+    bool tile_fused = true;                    // tile path: raster and resolve in one launch (S3R_TILE_FUSED=0: two)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -646,7 +645,7 @@ void initialize() {
         const char *bb = getenv("S3R_TILE_BIN_BUDGET_MB");
         if (bb && atoll(bb) > 0) g.tile_bin_budget = (uint64_t)atoll(bb) << 20;
         const char *f = getenv("S3R_TILE_FUSED");
-        g.tile_fused = f ? (atoi(f) != 0 ? 1 : 0) : -1;
+        g.tile_fused = !(f && atoi(f) == 0);
     }
     for (int id : ids) {
         Dev *d = new Dev();
@@ -898,11 +897,10 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     const uint32_t th = tile_height(), tyn = (rows_local + th - 1) / th;
     uint32_t slabs = frame_rows ? g.tile_slabs : 1u;
     slabs = std::max(1u, std::min({slabs, tyn, kMaxTileSlabs}));
-    // fused raster + resolve: whole frames by default -- stress scene, one MI355X
-    // (profiles/r04_tile_fused_ab.txt): whole frame 800 -> 854 fps in HBM, delivered 583 -> 614; part 0
-    // of 8 4 328 -> 4 026 (its longer-lived workgroups hold slots the next frame's setup, the part's
-    // bound, runs in)
-    const bool fused = g.tile_fused == 1 || (g.tile_fused < 0 && nparts == 1);
+    // fused raster + resolve -- stress scene, one MI355X: whole frame 800 -> 854 fps in HBM, delivered
+    // 583 -> 614 (lists, profiles/r04_tile_fused_ab.txt); part 0 of 8 4 328 -> 4 026 with the lists,
+    // but 4 491-4 632 -> 4 672-4 696 with the bins (profiles/r04_part8_ab.txt), so for every frame
+    const bool fused = g.tile_fused;
     const size_t npx = (size_t)W * rows_local;
     if (d.deferred_cap < npx) {                // pixels whose winner needs its full setup (either way)
         HIPCHECK(hipDeviceSynchronize());
