@@ -56,7 +56,9 @@ def parse():
     p.add_argument('--height', type=int, default=2160)
     p.add_argument('--scene', default='full')
     p.add_argument('--pose', default='P_over')
-    p.add_argument('--band', type=int, default=16, help='rows per interleaved band (multi-GPU)')
+    p.add_argument('--band', type=int, default=0,
+                   help='rows per interleaved band (multi-GPU); 0: the library\'s choice by fragment path '
+                        '(s3r_frame_band: 16 on the row path, two bands per GPU on the tile path)')
     p.add_argument('--devices', default=None,
                    help='comma-separated device ids behind updateAndRender (default 0..N-1; ids may repeat '
                         'to rehearse N parts on one GPU)')
@@ -296,18 +298,21 @@ def run_rank0(a, N, np, torch):
     nt = min(steps, MIN_TIMED)
     for _ in range(nt):
         call(hold_in)
-    dl_frag_ms, dl_frame_ms, dl_nfr = r.timing_collect()
+    st_dl = r.timing_stages()
+    dl_frag_ms, dl_frame_ms, dl_nfr, dl_geo_ms = st_dl['frag_ms'], st_dl['frame_ms'], st_dl['frames'], st_dl['geo_ms']
     r.timing(False)
 
     counts = r.scene_counts()      # V, I, A, texels, slots, tile pairs, path
     nv, ni, na, ntex, nslots, pairs, path = counts[:7]
+    B = B or r.frame_band(H, len(devices))          # (the library's choice, now that the path is known)
     rows0 = r.lib.s3r_band_rows_local(H, B, len(devices), 0) if len(devices) > 1 and H > B else H
 
     def kernel_bytes(rows):
         if path == 2:
-            # tile path, fragment stage = k_tile_raster + k_tile_resolve: framebuffer rows, the per-pixel
-            # (1/z, slot) keys written and read back, and per (slot, tile) pair its list entry + 64-B record
-            return 'k_tile_raster+k_tile_resolve', 4 * W * rows + 16 * W * rows + (4 + RASTER_REC_BYTES) * pairs
+            # tile path, fragment stage = k_tile_raster<true> (raster and shading fused) + the short
+            # k_tile_resolve_deferred: the framebuffer rows, and per binned (slot, tile) entry its 4-B bin
+            # entry and 64-B raster record read (pairs: the frame's binned entries, s3r_scene_counts)
+            return 'k_tile_raster<true> (fused) + k_tile_resolve_deferred', 4 * W * rows + (4 + RASTER_REC_BYTES) * pairs
         # row path, k_fragment: the framebuffer rows + the ripmap texels it may sample + the triangle
         # setup records it reads
         return 'k_fragment', 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
@@ -315,7 +320,7 @@ def run_rank0(a, N, np, torch):
     # device-resident rate of one GPU: whole frames pipelined into HBM (no host copy), and the HBM
     # roofline of the fragment kernel from HIP events on its stream in a second pass of those frames
     device_fps = None
-    frag_ms, frame_ms, nfr, roof_rows, roof_launch = dl_frag_ms, dl_frame_ms, dl_nfr, rows0, 'delivered frames'
+    frag_ms, frame_ms, nfr, geo_ms, roof_rows, roof_launch = dl_frag_ms, dl_frame_ms, dl_nfr, dl_geo_ms, rows0, 'delivered frames'
     if not a.no_device:
         r.configure_devices([], B)
         r.configure(data_path, devices[0])
@@ -334,7 +339,8 @@ def run_rank0(a, N, np, torch):
         r.timing(True)
         for _ in range(nt):
             r.render_bands(hold_in, W, H, H, 1, 0, out.data_ptr(), stream.cuda_stream)
-        frag_ms, frame_ms, nfr = r.timing_collect()
+        st_dv = r.timing_stages()
+        frag_ms, frame_ms, nfr, geo_ms = st_dv['frag_ms'], st_dv['frame_ms'], st_dv['frames'], st_dv['geo_ms']
         r.timing(False)
         roof_rows, roof_launch = H, 'whole frame into HBM, frames pipelined (device_fps pass)'
         del out
@@ -398,11 +404,19 @@ def run_rank0(a, N, np, torch):
         'host_buffer': {'halves_pinned': halves_pinned, 'pinned_frames': host['pinned_frames'],
                         'pageable_frames': host['pageable_frames']},
         'device_fps': round(device_fps, 3) if device_fps else None,
-        'device_frame_ms': round(frame_ms / max(nfr, 1), 5),
+        'device_frame_ms': round(1e3 / device_fps, 5) if device_fps else None,
+        # HIP events from a frame's first launch to its fragment stage's end (frames pipelined: includes
+        # the wait behind earlier frames' stages)
+        'device_frame_latency_ms': round(frame_ms / max(nfr, 1), 5),
         'fragment_kernel_ms': round(frag_avg_s * 1e3, 5),
         'fragment_kernel_ms_delivered': round(dl_frag_ms / max(dl_nfr, 1), 5),
-        # tile path: the per-triangle stages (cluster cull, setup, scan, fill) = device frame - fragment stage
-        'setup_fill_ms': round((frame_ms - frag_ms) / max(nfr, 1), 5) if path == 2 else None,
+        # the geometry stage (row path: k_geometry; tile path: cluster cull, setup, clip and binning), HIP
+        # events on its stream from the frame's first launch to the stage's end, same frames as roofline
+        'setup_ms': round(geo_ms / max(nfr, 1), 5),
+        'setup_bytes_per_frame': (16 * nv + 4 * ni + 4 * pairs) if path == 2 else None,
+        'setup_bytes_note': ('tile path, a lower bound: vertices 16 B and indices 4 B read, a 4-B bin entry '
+                             'written per binned entry; the 64-B raster record of each live slot is not counted '
+                             '(bins mode does not count live slots)') if path == 2 else None,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
                      'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,

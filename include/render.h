@@ -53,7 +53,8 @@ int s3r_configure(const char *data_path, int device);
 
 /* Several GPUs behind updateAndRender (the reference's one call per frame, main.swift:121 ->
  * render.cpp:264-265, from one thread).  With n_devices > 1, every updateAndRender splits the
- * frame's rows into interleaved bands of band_rows rows (0: S3R_BAND or 16) -- frame row y belongs to
+ * frame's rows into interleaved bands of band_rows rows (0: S3R_BAND, else by fragment path,
+ * s3r_frame_band) -- frame row y belongs to
  * device ((y / band_rows) % n_devices) -- and each device renders its bands and copies them
  * straight into their rows of pixel_data->buffer over its own PCIe link, device 0 on the calling
  * thread and the others on one library worker thread each; the call returns when every part has
@@ -62,6 +63,10 @@ int s3r_configure(const char *data_path, int device);
  * binds updateAndRender (the Swift app), S3R_DEVICES="0,1,2,..." selects the devices instead.  Drops
  * all state like s3r_configure.  Returns 0, or -1 on bad arguments (negative id, n_devices > 64). */
 int s3r_configure_devices(const int *device_ids, int n_devices, uint32_t band_rows);
+/* Rows per band updateAndRender uses for a frame of `height` rows over n_parts devices (after
+ * s3r_configure / the first frame, which fix the fragment path): the configured band_rows, else 16 on
+ * the row path and ceil(height / (2 n_parts)) on the tile path (two bands per device). */
+uint32_t s3r_frame_band(uint32_t height, uint32_t n_parts);
 
 /* The devices updateAndRender uses (after init: the ones in use); writes up to max_ids ids and
  * returns the count. */
@@ -166,6 +171,9 @@ uint32_t s3r_band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_par
  * out[0] = summed fragment-kernel ms, out[1] = summed frame ms, out[2] = frames, and resets. */
 void s3r_timing(int enable);
 void s3r_timing_collect(double out[3]);
+/* The same plus out[3] = summed ms of the frames' geometry / setup stage (from the frame's first
+ * launch to the end of k_geometry, or of the tile path's setup and binning). */
+void s3r_timing_stages(double out[4]);
 
 /* Scene counts after init: out = {vertices, indices, attributes, texels, triangle slots,
  * (slot, tile) pairs binned in the last frame (tile path), the last frame's path (1 rows, 2 tiles),

@@ -2170,7 +2170,6 @@ __global__ void __launch_bounds__(64) k_tile_bins_done(uint32_t *__restrict__ ct
         ctr[0] = 0u; ctr[1] = 0u; ctr[2] = kept; ctr[3] = 0u; ctr[5] = need;
         if (sum_host) {
             __hip_atomic_store(sum_host + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(sum_host + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(sum_host + 3, kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(sum_host + 4, need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(sum_host, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2314,7 +2313,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
     // set's next frame -- unless the list overflowed (the frame's fill runs again, render_api.cpp)
-    if (tile0 == 0u && blockIdx.x == 0u && threadIdx.x < kTileShards && *total <= cap)
+    if (!bin_cap && tile0 == 0u && blockIdx.x == 0u && threadIdx.x < kTileShards && *total <= cap)
         *shard_ctr(ctr, 1, threadIdx.x) = 0u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = tile0 + blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
@@ -2347,6 +2346,9 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         }
         __syncthreads();
         n = ls.zwave[0];
+        // the frame's binned entries, for the statistics (bins mode has no list length): summed per
+        // shard in the live counters, which bins mode leaves unused; k_tile_resolve_deferred totals them
+        if (tid == 0u && n) atomicAdd(shard_ctr(ctr, 1, tile % kTileShards), n);
     } else {
         // a list longer than its buffer (overflow, see k_tile_fill) is incomplete: the frame is redone
         const uint32_t ntiles = tiles_x * ((rows_local + kTileH - 1u) / kTileH);
@@ -2572,8 +2574,22 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
 // The fused raster's deferred pixels (ctr[3] entries {out index, key, x | y << 16}): shaded with the
 // winner's full setup.  Grid-stride (the queue is short: pixels of near-plane and clip-appended
 // winners).
+// Bins mode (bins != 0): workgroup 0 also totals the frame's binned entries from the raster's per-shard
+// sums (resetting them) into ctr[1] and, when given, word 2 of the host summary (system scope; the
+// host reads it once the frame is done).
 __global__ void __launch_bounds__(256) k_tile_resolve_deferred(ShadeScene sc, const uint4 *__restrict__ deferred,
-                                                               const uint32_t *__restrict__ ctr, uint32_t *__restrict__ out) {
+                                                               uint32_t *__restrict__ ctr, uint32_t *__restrict__ out,
+                                                               uint32_t bins, uint32_t *__restrict__ sum_host) {
+    if (bins && blockIdx.x == 0 && threadIdx.x < 64u) {
+        static_assert(kTileShards == 64, "one lane per shard");
+        uint32_t v = *shard_ctr(ctr, 1, threadIdx.x);
+        *shard_ctr(ctr, 1, threadIdx.x) = 0u;
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+        if (threadIdx.x == 0) {
+            ctr[1] = v;
+            if (sum_host) __hip_atomic_store(sum_host + 2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const uint32_t n = ctr[3];
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint4 e = deferred[i];
@@ -3080,7 +3096,7 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows, uint32_t *counts,
-                                uint32_t bin_cap, uint32_t xoff) {
+                                uint32_t bin_cap, uint32_t xoff, uint32_t *sum_host) {
     const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
@@ -3088,8 +3104,8 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                        nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr,
                        (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred,
                        counts, bin_cap, xoff);
-    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred,
-                       (const uint32_t *)ctr, out);
+    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred, ctr, out,
+                       bin_cap ? 1u : 0u, sum_host);
 }
 
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
@@ -3109,9 +3125,11 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
 void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
                                   const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
                                   const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
-                                  uint32_t *out, const uint4 *deferred, const uint32_t *ctr, hipStream_t st) {
+                                  uint32_t *out, const uint4 *deferred, uint32_t *ctr, hipStream_t st, bool bins,
+                                  uint32_t *sum_host) {
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
-    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, deferred, ctr, out);
+    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, deferred, ctr, out, bins ? 1u : 0u,
+                       sum_host);
 }
 
 }  // namespace s3r

@@ -64,7 +64,7 @@ using namespace s3r;
 
 namespace {
 
-struct TimingSlot { hipEvent_t frame0, frag0, frag1; };
+struct TimingSlot { hipEvent_t frame0, geo1, frag0, frag1; };   // geo1: the frame's geometry / setup stage done
 
 // Per-frame buffer sets in flight: frame k's geometry writes set k % kSets once the fragment kernel
 // of frame k - kSets (the set's last reader) is done, on geometry stream k % kGeoStreams, so the
@@ -351,7 +351,7 @@ struct Lib {
     bool timing = false;
 
     std::vector<Dev *> devs;                   // devs[0]: s3r_render_bands' device, updateAndRender's first
-    uint32_t band = kDefaultBand;              // resolved band_rows
+    uint32_t band = 0;                         // resolved band_rows (0: per frame, frame_band)
     Pool pool;
 
     // caller buffers registered as pinned memory (the double buffer: main.swift:117-118, :164):
@@ -632,7 +632,7 @@ void initialize() {
     g.band = g.band_rows;
     if (!g.band) {
         const char *e = getenv("S3R_BAND");
-        g.band = e && atoi(e) > 0 ? (uint32_t)atoi(e) : kDefaultBand;
+        g.band = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 0u;
     }
     g.serial = getenv("S3R_SERIAL") != nullptr;
     {
@@ -776,7 +776,8 @@ TimingSlot *timing_slot(Dev &d) {
     if (!g.timing) return nullptr;
     if (d.tcount == d.tslots.size()) {
         TimingSlot t;
-        HIPCHECK(hipEventCreate(&t.frame0)); HIPCHECK(hipEventCreate(&t.frag0)); HIPCHECK(hipEventCreate(&t.frag1));
+        HIPCHECK(hipEventCreate(&t.frame0)); HIPCHECK(hipEventCreate(&t.geo1));
+        HIPCHECK(hipEventCreate(&t.frag0)); HIPCHECK(hipEventCreate(&t.frag1));
         d.tslots.push_back(t);
     }
     return &d.tslots[d.tcount++];
@@ -859,6 +860,21 @@ bool use_tile_path() {
     return 2ull * g.ntri > kRowPathMaxSlots;
 }
 
+// Rows per interleaved band of an H-row frame split over nparts devices: the configured band
+// (s3r_configure_devices, S3R_BAND), else by fragment path.  Row path: 16 rows (its fragment
+// workgroups are 4-row blocks of 384-px bins; the floor and sky rows spread evenly).  Tile path:
+// two bands per part, ceil(H / 2N) rows -- a part's cluster cull keeps the clusters that reach its
+// bands, and an icosahedron of the stress scene (17-27 rows tall) meets ~(band + 22) / (N band) of
+// them: part 0 of 8 at 4K (config 5), one MI355X, 16-row bands 4 539-4 663 fps, 54: 5 322, 135:
+// 5 855, 270 (one contiguous band): 6 015 (profiles/r04_band_sweep.txt).  Two bands rather than one
+// keep some balance for scenes that are not uniform across the frame.
+uint32_t frame_band(uint32_t H, uint32_t nparts) {
+    if (g.band) return g.band;
+    if (nparts <= 1) return H ? H : 1u;
+    if (!use_tile_path()) return kDefaultBand;
+    return std::max(kDefaultBand, (H + 2 * nparts - 1) / (2 * nparts));
+}
+
 // The device's clusters as the tile kernels take them for a frame of nparts parts (ncl 0: no cull).
 // S3R_CLUSTERS: 0 never, 1 (default) for frame parts only -- a whole frame in view keeps nearly every
 // cluster, and the cull's records cost more than they save there (stress scene, one MI355X: whole
@@ -887,6 +903,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     uint32_t *bcounts = bins ? d.tile_counts[p] : nullptr;
     const uint32_t bcap = bins ? d.bin_cap : 0u;
     HIPCHECK(hipEventRecord(d.geo_done[p], geo));
+    if (ts) HIPCHECK(hipEventRecord(ts->geo1, geo));
     follow_previous_frame(d, st);
     HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
@@ -911,7 +928,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     if (fused) {
         launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                    d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
-                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff);
+                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff,
+                                   d.tile_sum_dev + kSumWords * p);
     } else if (slabs == 1u) {
         launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list, d.keys,
                            d.tile_list_cap[p], st, 0, 0xFFFFFFFFu, bcounts, bcap, d.tile_xoff);
@@ -919,7 +937,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                             sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
                             g.tile_line_grid, d.deferred, d.tile_ctr[p]);
         launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], st);
+                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], st, bins, d.tile_sum_dev + kSumWords * p);
     } else {
         if (!d.res_stream) {
             HIPCHECK(hipSetDevice(d.device));
@@ -938,7 +956,8 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
                                 ty0 * th, std::min(rows_local, ty1 * th), g.tile_line_grid, d.deferred, d.tile_ctr[p]);
         }
         launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], d.res_stream);
+                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], d.res_stream, bins,
+                                     d.tile_sum_dev + kSumWords * p);
         HIPCHECK(hipEventRecord(d.res_done, d.res_stream));
         HIPCHECK(hipStreamWaitEvent(st, d.res_done, 0));
     }
@@ -1323,6 +1342,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
                     lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts);
     d.hp.lap(3);
+    if (ts) HIPCHECK(hipEventRecord(ts->geo1, geo));
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first
     // workgroup reports the previous fragment launch complete (wait_set_free); the completion event
     // only where S3R_SERIAL waits on it.  The fragment workgroups reset their bins' pair counts: the
@@ -1991,7 +2011,7 @@ void fill_adapt(const FillJob &job, uint32_t nparts) {
     else if (-g.fill_skew_us > F && g.fill_gpu > 0) { g.fill_gpu--; g.fill_skew_us = 0; }
 }
 
-MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t nparts, bool fill) {
+MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, bool fill) {
     const Lib::Reg *reg = find_reg(buffer, (size_t)W * H * 4);
     DirectDelivery dd{};
     for (uint32_t i = 0; i < nparts; i++) {
@@ -2030,7 +2050,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t npa
             g.fill_placed = !cpus.empty();
         }
     }
-    const uint32_t band = nparts == 1 ? H : g.band;
+    if (nparts == 1) band = H;
     for (uint32_t i = 0; i < nparts; i++) {                 // the parts' bin layouts
         FillPart &fp = job.parts[i];
         fp.rows_local = nparts == 1 ? H : band_rows_local(H, band, nparts, i);
@@ -2164,8 +2184,9 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
     // several devices: each renders its interleaved bands and copies them into their rows (a caller
     // buffer smaller than the frame -- not the reference's usage -- takes the one-device path)
     const uint32_t ndev = (uint32_t)g.devs.size();
-    const uint32_t nparts = (ndev > 1 && copy_bytes == frame_bytes && H > g.band) ? ndev : 1u;
-    Delivery job{W, H, g.band, nparts, pixel_data->buffer, copy_bytes, false};
+    const uint32_t band = frame_band(H, ndev);
+    const uint32_t nparts = (ndev > 1 && copy_bytes == frame_bytes && H > band) ? ndev : 1u;
+    Delivery job{W, H, band, nparts, pixel_data->buffer, copy_bytes, false};
     bool pinned = false;
     if (copy_bytes) pinned = host_pinned(pixel_data->buffer, pixel_data->bufferSize);
     const int mode = delivery_mode();
@@ -2175,7 +2196,7 @@ __attribute__((visibility("default"))) void updateAndRender(const PixelData *pix
         const bool fill = (mode == kFill || mode == kAuto) && !use_tile_path();
         const Lib::Reg *reg = find_reg(pixel_data->buffer, frame_bytes);
         const bool unmapped = reg && g.unmapped_epoch == g.reg_epoch && g.unmapped_a == reg->a;
-        const MappedResult mr = unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, nparts, fill);
+        const MappedResult mr = unmapped ? kUnmapped : mapped_frame(pixel_data->buffer, W, H, band, nparts, fill);
         if (mr == kMapped) {
             g.pinned_frames++;
             for (size_t i = frame_bytes / 4; i < pixel_data->bufferSize / 4; i++) pixel_data->buffer[i] = kBackground;
@@ -2229,6 +2250,10 @@ __attribute__((visibility("default"))) int s3r_configure_devices(const int *devi
     g.device_ids.assign(device_ids, device_ids + n_devices);
     g.band_rows = band_rows;
     return 0;
+}
+
+__attribute__((visibility("default"))) uint32_t s3r_frame_band(uint32_t height, uint32_t n_parts) {
+    return frame_band(height, n_parts);
 }
 
 __attribute__((visibility("default"))) int s3r_devices(int *out_ids, int max_ids) {
@@ -2406,19 +2431,21 @@ __attribute__((visibility("default"))) void s3r_timing(int enable) {
     for (Dev *d : g.devs) d->tcount = 0;
 }
 
-__attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
-    double frag = 0, frame = 0;
+__attribute__((visibility("default"))) void s3r_timing_stages(double out[4]) {
+    double frag = 0, frame = 0, geo = 0;
     size_t n = 0;
     if (!g.devs.empty()) {
         Dev &d = *g.devs[0];
         HIPCHECK(hipSetDevice(d.device));
         for (size_t i = 0; i < d.tcount; i++) {
-            float a = 0, b = 0;
+            float a = 0, b = 0, c = 0;
             HIPCHECK(hipEventSynchronize(d.tslots[i].frag1));
             HIPCHECK(hipEventElapsedTime(&a, d.tslots[i].frag0, d.tslots[i].frag1));
             HIPCHECK(hipEventElapsedTime(&b, d.tslots[i].frame0, d.tslots[i].frag1));
+            HIPCHECK(hipEventElapsedTime(&c, d.tslots[i].frame0, d.tslots[i].geo1));
             frag += a;
             frame += b;
+            geo += c;
         }
         n = d.tcount;
         for (Dev *e : g.devs) e->tcount = 0;
@@ -2426,6 +2453,13 @@ __attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
     out[0] = frag;
     out[1] = frame;
     out[2] = (double)n;
+    out[3] = geo;
+}
+
+__attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
+    double o[4];
+    s3r_timing_stages(o);
+    out[0] = o[0]; out[1] = o[1]; out[2] = o[2];
 }
 
 __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {

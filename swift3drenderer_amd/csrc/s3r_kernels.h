@@ -166,7 +166,8 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows,
-                                uint32_t *counts = nullptr, uint32_t bin_cap = 0, uint32_t xoff = 0);
+                                uint32_t *counts = nullptr, uint32_t bin_cap = 0, uint32_t xoff = 0,
+                                uint32_t *sum_host = nullptr);      // bins: the entries' total (launch_tile_resolve_deferred)
 void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
                          const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
                          uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
@@ -179,7 +180,9 @@ void launch_tile_resolve(const unsigned long long *keys, const void *recs, const
 void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
                                   const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,
                                   const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex, uint32_t ntex,
-                                  uint32_t *out, const uint4 *deferred, const uint32_t *ctr, hipStream_t st);   // frame_rows: wave stores on the caller's 64-B line grid
+                                  uint32_t *out, const uint4 *deferred, uint32_t *ctr, hipStream_t st,
+                                  bool bins = false,                   // bins mode: also total the binned entries
+                                  uint32_t *sum_host = nullptr);       // (into ctr[1] and word 2 of sum_host)
 
 // The N parts of an interleaved band split, gathered one after another (part p's compact rows from
 // row p * part_stride_rows), written into the W x H frame in frame-row order (one launch).

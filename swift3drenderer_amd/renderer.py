@@ -121,6 +121,13 @@ class Renderer:
         if self.lib.s3r_configure_devices(ids, len(device_ids), band) != 0:
             raise ValueError(f'bad device list {device_ids!r}')
 
+    def frame_band(self, height: int, nparts: int) -> int:
+        """Rows per band of an updateAndRender frame over nparts devices (include/render.h s3r_frame_band)."""
+        f = self.lib.s3r_frame_band
+        f.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        f.restype = ctypes.c_uint32
+        return int(f(height, nparts))
+
     def devices(self):
         out = (ctypes.c_int * 64)()
         n = self.lib.s3r_devices(out, 64)
@@ -244,6 +251,13 @@ class Renderer:
         out = (ctypes.c_double * 3)()
         self.lib.s3r_timing_collect(out)
         return out[0], out[1], int(out[2])
+
+    def timing_stages(self) -> dict:
+        """Summed HIP-event ms since timing(True) (include/render.h s3r_timing_stages): fragment
+        stage, whole frame, geometry / setup stage, and the frame count; resets like timing_collect."""
+        out = (ctypes.c_double * 4)()
+        self.lib.s3r_timing_stages(out)
+        return {'frag_ms': out[0], 'frame_ms': out[1], 'frames': int(out[2]), 'geo_ms': out[3]}
 
     def scene_counts(self):
         out = (ctypes.c_uint64 * 8)()
