@@ -562,8 +562,7 @@ void dev_init(Dev &d, const HostScene &s) {
     d.disc = dalloc<uint8_t>(g.na);
     d.vidx = dalloc<uint32_t>(3 * (size_t)ntri); d.aidx = dalloc<uint32_t>(3 * (size_t)ntri);
     d.tex = dalloc<uint32_t>(g.ntex);
-    for (int p = 0; p < kSets; p++) {
-        d.tris[p] = dalloc<TriSetup>(2 * (size_t)ntri);
+    for (int p = 0; p < kSets; p++) {           // (the row path's TriSetup records: ensure_row_sets)
         HIPCHECK(hipEventCreateWithFlags(&d.geo_done[p], hipEventDisableTiming));
         HIPCHECK(hipEventCreateWithFlags(&d.frag_done[p], hipEventDisableTiming));
     }
@@ -1009,6 +1008,20 @@ void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
 // (S3R_TILE_BIN_BUDGET_MB, 32 GiB for all buffer sets) the device drops its bins and uses the lists.
 bool bins_on(const Dev &d) { return g.tile_bins && !d.bins_off; }
 
+// Per-path storage, allocated on a path's first frame (the other path's would be wasted: the row path's
+// 240-B TriSetup per slot is 38 GB for the four buffer sets of the 20 M-triangle stress scene, which
+// only the tile path renders; the lists' 16-B live entries are 2.6 GB that bins mode never touches).
+void ensure_row_sets(Dev &d) {
+    if (d.tris[0]) return;
+    HIPCHECK(hipDeviceSynchronize());
+    for (int p = 0; p < kSets; p++) d.tris[p] = dalloc<TriSetup>(2 * (size_t)g.ntri);
+}
+void ensure_live(Dev &d) {
+    if (d.live[0]) return;
+    HIPCHECK(hipDeviceSynchronize());
+    for (int p = 0; p < kSets; p++) d.live[p] = dalloc<uint4>((size_t)2 * g.ntri);
+}
+
 void drop_bins(Dev &d) {
     HIPCHECK(hipDeviceSynchronize());
     for (int q = 0; q < kSets; q++) {
@@ -1104,6 +1117,7 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
     const uint64_t nt = tile_slots(W, rows_local, d.tile_xoff);
     while (sum[4] != 0) {
         const bool bins = grow_bins(d, sum[4]);
+        if (!bins) ensure_live(d);
         HIPCHECK(hipMemsetAsync(d.tile_counts[p], 0, nt * sizeof(uint32_t), geo));
         __atomic_store_n(&d.tile_sum_host[kSumWords * p], 0u, __ATOMIC_RELEASE);   // (the earlier pass carried this tag)
         launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, (float)W, (float)H, W, band, nparts, part, rows_local,
@@ -1172,7 +1186,6 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (!d.recs[0]) {
         for (int p = 0; p < kSets; p++) {
             d.recs[p] = dalloc<uint8_t>((size_t)2 * g.ntri * raster_rec_bytes());
-            d.live[p] = dalloc<uint4>((size_t)2 * g.ntri);
             if (!d.clipq) d.clipq = dalloc<uint32_t>(g.ntri);
             d.tile_ctr[p] = dalloc<uint32_t>(kTileCtrWords);
             HIPCHECK(hipMemset(d.tile_ctr[p], 0, kTileCtrWords * sizeof(uint32_t)));
@@ -1192,6 +1205,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     const TileClusters cl = tile_clusters(d, nparts);
     if (bins_on(d)) ensure_bins(d, nt);
     const bool bins = bins_on(d);
+    if (!bins) ensure_live(d);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
@@ -1262,6 +1276,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
         return;
     }
     d.last_path = 1;
+    ensure_row_sets(d);
     fragment_configure(W, rows_local);
     const size_t need = (size_t)2 * g.ntri * rows_local * start_entries(W) * 4;
     if (d.rowtab_cap < need) {
