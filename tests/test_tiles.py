@@ -78,6 +78,30 @@ def test_stress_small_matches_oracle(gpu_renderer, icosa_dir, pose, w, h):
     assert np.array_equal(got, want), diff(got, want)
 
 
+def test_frame_band_by_path(gpu_renderer, icosa_dir, scene_dir, monkeypatch):
+    """s3r_frame_band: updateAndRender's rows per band over N devices -- 16 on the row path, two bands
+    per device on the tile path (ceil(H / 2N), at least 16), the configured band when one is given,
+    the whole frame for one device."""
+    r = gpu_renderer
+    try:
+        r.configure(icosa_dir[2000])
+        r.update_and_render(640, 480, (0, 0, 0, 0, 0, 0))
+        assert r.raster_path() == 'tiles'
+        assert [r.frame_band(2160, n) for n in (1, 2, 4, 8)] == [2160, 540, 270, 135]
+        assert r.frame_band(4320, 8) == 270 and r.frame_band(100, 8) == 16
+        r.configure(scene_dir['full'])
+        r.update_and_render(640, 480, (0, 0, 0, 0, 0, 0))
+        assert r.raster_path() == 'rows'
+        assert r.frame_band(2160, 8) == 16
+        r.configure_devices([0, 0], 24)
+        r.configure(scene_dir['full'])
+        r.update_and_render(640, 480, (0, 0, 0, 0, 0, 0))
+        assert r.frame_band(2160, 2) == 24
+    finally:
+        r.configure_devices([])
+        r.configure(None)
+
+
 @pytest.mark.parametrize('clusters', ['2', '1', '0'])
 def test_stress_100k_4k_matches_oracle(gpu_renderer, icosa_dir, oracle_100k_4k, monkeypatch, clusters):
     """100 000 icosahedra (2 M triangles) at 3840x2160 -- a tenth of config 5, oracle-checkable --
