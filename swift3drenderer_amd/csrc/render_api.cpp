@@ -151,16 +151,13 @@ struct Dev {
     // host-coherent, per buffer set: {tag, live entries, list length, cluster-kept positions}, written
     // by k_tile_cursor as soon as they are known (tag = the frame's number)
     uint32_t *tile_sum_host = nullptr, *tile_sum_dev = nullptr;
-    // synchronous tile-path frames (or sub-parts of one) not yet checked for a list / bin overflow
-    // (tile_redo_if_overflowed, after the frame's stream has drained)
-    struct TilePending {
-        uint32_t set, W, H, band, nparts, part, rows, xoff;
-        uint32_t *out;
-        bool bins, frame_rows;
-    } tile_pend[kSets];
-    uint32_t tile_npend = 0;
+    // a synchronous tile-path frame awaiting its overflow check (tile_redo_if_overflowed): its set
+    // and what its fragment stage needs to run again
+    bool tile_pending = false, tile_pending_bins = false;
     uint32_t tile_xoff = 0;                    // the current frame's tile-grid shift (tile_xoff_for)
-    uint32_t tile_H = 0;                       // the current tile-path frame's height
+    uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
+    uint32_t *tile_out = nullptr;
+    bool tile_frame_rows = false;
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     uint64_t last_live = 0, last_kept = 0;     // tile path, last read-back frame: live slots, cluster-kept triangles
@@ -350,7 +347,6 @@ struct Lib {
     bool tile_bins = true;                     // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
     uint64_t tile_bin_budget = 32ull << 30;    // bytes of bins per device, all buffer sets (S3R_TILE_BIN_BUDGET_MB)
     bool tile_fused = true;                    // tile path: raster and resolve in one launch (S3R_TILE_FUSED=0: two)
-    uint32_t tile_split = 1;                   // tile path, delivered whole frames: sub-frames (S3R_TILE_SPLIT)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -649,8 +645,6 @@ void initialize() {
         if (bb && atoll(bb) > 0) g.tile_bin_budget = (uint64_t)atoll(bb) << 20;
         const char *f = getenv("S3R_TILE_FUSED");
         g.tile_fused = !(f && atoi(f) == 0);
-        const char *sp = getenv("S3R_TILE_SPLIT");
-        g.tile_split = sp && atoi(sp) > 1 ? std::min<uint32_t>((uint32_t)atoi(sp), kSets) : 1u;
     }
     for (int id : ids) {
         Dev *d = new Dev();
@@ -1079,39 +1073,37 @@ bool grow_bins(Dev &d, uint32_t need) {
 void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
            uint32_t rows_local, hipStream_t geo);
 
-bool tile_redo_one(Dev &d, const Dev::TilePending &e, hipStream_t st) {
-    const uint32_t p = e.set;
+bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
+    if (!d.tile_pending) return false;
+    d.tile_pending = false;
+    const uint32_t p = d.tile_pending_set;
     const volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     const uint64_t total = sum[2];
     d.last_pairs = total;
     d.last_live = sum[1];
     d.last_kept = sum[3];
-    d.tile_H = e.H;
-    d.tile_xoff = e.xoff;
-    hipStream_t geo = d.geo[0];
-    if (e.bins) {
+    if (d.tile_pending_bins) {
         if (sum[4] == 0) return false;
         // a (tile, bucket) outgrew its bin: bin the frame again into larger bins (or, past the budget,
         // into the lists), then its fragment stage
         d.tile_overflows++;
-        rebin(d, p, e.W, e.H, e.band, e.nparts, e.part, e.rows, geo);
-    } else {
-        if (total <= d.tile_list_cap[p]) return false;
-        d.tile_overflows++;
-        grow_tile_list(d, p, total);
-        launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], e.W, e.rows, d.tile_cursor[p], d.tile_ctr[p], geo, e.xoff);
+        hipStream_t geo = d.geo[0];
+        rebin(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
+        tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
+                            nullptr, d.tile_frame_rows);
+        HIPCHECK(hipStreamSynchronize(st));
+        return true;
     }
-    tile_fragment_stage(d, p, e.W, e.band, e.nparts, e.part, e.rows, e.out, geo, st, nullptr, e.frame_rows);
+    if (total <= d.tile_list_cap[p]) return false;
+    d.tile_overflows++;
+    grow_tile_list(d, p, total);
+    hipStream_t geo = d.geo[0];
+    launch_tile_cursor(d.tile_counts[p], d.tile_offs[p], d.tile_W, d.tile_rows, d.tile_cursor[p], d.tile_ctr[p], geo,
+                       d.tile_xoff);
+    tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
+                        nullptr, d.tile_frame_rows);
     HIPCHECK(hipStreamSynchronize(st));
     return true;
-}
-
-bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
-    const uint32_t n = d.tile_npend;
-    d.tile_npend = 0;
-    bool redone = false;
-    for (uint32_t i = 0; i < n; i++) redone |= tile_redo_one(d, d.tile_pend[i], st);
-    return redone;
 }
 
 // Buffer set p's frame binned again after its bins overflowed (the summary's need in sum[4]), until it
@@ -1244,9 +1236,12 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     tile_fragment_stage(d, p, W, band, nparts, part, rows_local, out, geo, st, ts, frame_rows);
     if (sync) {
         // the overflow check reads this frame's summary once the frame is done
-        if (d.tile_npend < (uint32_t)kSets)
-            d.tile_pend[d.tile_npend++] = Dev::TilePending{p, W, H, band, nparts, part, rows_local, d.tile_xoff, out,
-                                                           bins && bins_on(d), frame_rows};
+        d.tile_pending = true;
+        d.tile_pending_bins = bins && bins_on(d);
+        d.tile_pending_set = p;
+        d.tile_W = W; d.tile_band = band; d.tile_nparts = nparts; d.tile_part = part; d.tile_rows = rows_local;
+        d.tile_out = out;
+        d.tile_frame_rows = frame_rows;
     }
 }
 
@@ -1273,26 +1268,10 @@ struct HostFill {
 // itself -- nothing could overlap it, and stream order replaces the cross-stream event (~9 us per
 // frame measured); otherwise it runs on a geometry stream so later frames' geometry overlaps
 // earlier frames' fragment kernels.
-uint32_t band_rows_local(uint32_t height, uint32_t band_rows, uint32_t n_parts, uint32_t part);
-
 void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st, const HostFill *hf = nullptr, bool sync = false) {
     TimingSlot *ts = timing_slot(d);
     if (use_tile_path()) {
-        // a whole frame written into the caller's buffer (S3R_TILE_SPLIT = k > 1): k sub-frames of
-        // contiguous rows, each culled to its rows by the clusters, issued one after another -- the
-        // setups run on the geometry stream, the fragment stages on st, so sub-frame i + 1's setup
-        // runs while sub-frame i's link-bound raster streams its rows to the host
-        const uint32_t k = hf && sync && nparts == 1 && H >= 32u * g.tile_split && tile_clusters(d, 2).ncl ? g.tile_split : 1u;
-        if (k > 1) {
-            const uint32_t b = (H + k - 1) / k;
-            for (uint32_t i = 0; i < k; i++) {
-                const uint32_t rows = band_rows_local(H, b, k, i);
-                if (rows) render_tiles(d, W, H, b, k, i, rows, out, st, i == 0 ? ts : nullptr, sync, true);
-            }
-            if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
-            return;
-        }
         render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts, sync, hf != nullptr);
         return;
     }

@@ -459,38 +459,6 @@ def test_tile_line_offsets_match_oracle(gpu_renderer, icosa_dir, devices):
         r.configure_devices([])
 
 
-@pytest.mark.parametrize('split,bin_cap', [('2', '256'), ('3', '4'), ('4', '256')])
-def test_tile_split_frames_match_oracle(gpu_renderer, icosa_dir, monkeypatch, split, bin_cap):
-    """Delivered whole frames as S3R_TILE_SPLIT sub-frames of contiguous rows, each culled to its rows
-    and issued one after another (render_api.cpp render_core), with overflowing bins (capacity 4)
-    binned again per sub-frame after the frame: the oracle's pixels, 640x480 and 1000x333."""
-    from oracle.oracle import OracleRenderer
-    monkeypatch.setenv('S3R_TILE_SPLIT', split)
-    monkeypatch.setenv('S3R_TILE_BIN_CAP', bin_cap)
-    r = gpu_renderer
-    path = icosa_dir[2000]
-    r.configure(path)
-    r.set_delivery('direct')
-    try:
-        o = OracleRenderer(path)
-        seq = ([(640, 480, (0, 0, 0, 0, 0, 0))] + [(640, 480, (40.0, 0, 0, 0, 0.0, 0.0))] * 5 +
-               [(1000, 333, (0, 0, 0, 0, 25.0, -10.0))] * 2)
-        keep = []
-        for k, (w, h, inp) in enumerate(seq):
-            half = np.empty((h, w), dtype=np.uint32)
-            keep.append(half)
-            half[:] = 0x5A5A5A5A
-            got = r.update_and_render(w, h, inp, half)
-            want = o.update_and_render(w, h, inp)
-            assert np.array_equal(got, want), f'frame {k} {w}x{h}: ' + diff(got, want)
-        assert r.raster_path() == 'tiles'
-        assert r.cluster_stats()['clusters'] > 0
-        if bin_cap == '4':
-            assert r.tile_stats()['overflows'] > 0
-    finally:
-        r.set_delivery('env')
-
-
 @pytest.mark.parametrize('bin_cap,budget_mb',[('256', ''), ('4', ''), ('4', '1'), ('256', '1')])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
 def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, budget_mb, devices):
