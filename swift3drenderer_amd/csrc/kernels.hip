@@ -2370,9 +2370,21 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
                 for (uint32_t step = 16; step >= 1u; step >>= 1)
                     if (ls.bstart[b + step] <= v) b += step;
                 s_nx = list[(size_t)(s0 + b) * bin_cap + (v - ls.bstart[b])];
+#ifdef S3R_BOUNDS
+                if (v - ls.bstart[b] >= bin_cap) {
+                    printf("S3R_BOUNDS raster: tile %u entry %u bucket %u start %u cap %u n %u\n", tile, v, b, ls.bstart[b], bin_cap, n);
+                    s_nx = 0;
+                }
+#endif
             } else {
                 s_nx = list[base + c + tid];
             }
+#ifdef S3R_BOUNDS
+            if (sc.ntri && s_nx >= 2u * sc.ntri) {
+                printf("S3R_BOUNDS raster: tile %u slot %u >= %u (bins %u)\n", tile, s_nx, 2u * sc.ntri, bin_cap);
+                s_nx = 0;
+            }
+#endif
             const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
             q0n = q[0]; q1n = q[1]; q2n = q[2]; q3n = q[3];
         }
@@ -2558,6 +2570,13 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             uint32_t v = kBackground;
             if (in) v = resolve_pixel<true>(sc, k, x, y);
             const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
+#ifdef S3R_BOUNDS
+            if (in && idx >= (size_t)W * (frame_rows ? (uint32_t)sc.sh : rows_local)) {
+                printf("S3R_BOUNDS fused store: tile %u x %u y %u lr %u idx %lu W %u rows %u\n", tile, x, y, lr,
+                       (unsigned long)idx, W, frame_rows ? (uint32_t)sc.sh : rows_local);
+                continue;
+            }
+#endif
             wave_append(in && v == kDeferPixel, make_uint4((uint32_t)idx, (uint32_t)k, (uint32_t)(k >> 32), (x & 0xFFFFu) | (y << 16)),
                         deferred, ctr + 3);
             if (in && v != kDeferPixel) out[idx] = v;
@@ -2594,6 +2613,12 @@ __global__ void __launch_bounds__(256) k_tile_resolve_deferred(ShadeScene sc, co
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint4 e = deferred[i];
         const unsigned long long k = (unsigned long long)e.y | ((unsigned long long)e.z << 32);
+#ifdef S3R_BOUNDS
+        if (e.x >= (uint32_t)sc.sw * (uint32_t)sc.sh || (uint32_t)(0xFFFFFFFFu - (uint32_t)k) >= 2u * sc.ntri) {
+            printf("S3R_BOUNDS deferred: %u of %u idx %u slot %u\n", i, n, e.x, 0xFFFFFFFFu - (uint32_t)k);
+            continue;
+        }
+#endif
         out[e.x] = resolve_pixel<false>(sc, k, e.w & 0xFFFFu, e.w >> 16);
     }
 }

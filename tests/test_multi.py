@@ -259,26 +259,40 @@ def test_gpu_deinterleave_matches_oracle(gpu_renderer, scene_dir, w, h, band, n)
 
 
 @pytest.mark.gpu
-def test_nccl_gather_one_rank(gpu_renderer, scene_dir):
-    """BandGather over torch.distributed's nccl backend (RCCL) in this process, world size 1: the RCCL
-    gather executes on the GPU and the frame comes out whole (this pool's boxes have one GPU; the
-    N-rank path is the same call)."""
+def test_nccl_gather_one_rank(scene_dir, tmp_path):
+    """BandGather over torch.distributed's nccl backend (RCCL), world size 1: the RCCL gather executes
+    on the GPU and the frame comes out whole (this pool's boxes have one GPU; the N-rank path is the
+    same call).  In a process of its own, as a rank is: the communicator's threads and memory stay out
+    of the test process (whose later GPU tests must not share a context with a torn-down RCCL)."""
+    import subprocess
+    import sys
     from oracle.oracle import render_pose
     from swift3drenderer_amd import poses
     w, h = 640, 480
     script = poses.script('P_over')
     want = render_pose(scene_dir['full'], script, w, h)
-    r = gpu_renderer
-    r.configure(scene_dir['full'])
-    for t in script:
-        r.update_and_render(w, h, t)
-    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{free_port()}', rank=0, world_size=1)
-    try:
-        bg = BandGather(w, h, 16, 1, 0, torch.device('cuda'))
-        r.render_bands(poses.hold('P_over'), w, h, 16, 1, 0, bg.send.data_ptr(),
-                       torch.cuda.current_stream().cuda_stream)
-        got = bg.gather()
-        torch.cuda.synchronize()
-    finally:
-        dist.destroy_process_group()
-    assert np.array_equal(got.cpu().numpy().view(np.uint32), want)
+    out = tmp_path / 'frame.npy'
+    code = f"""
+import numpy as np, torch, torch.distributed as dist
+from swift3drenderer_amd import poses
+from swift3drenderer_amd.multi import BandGather
+from swift3drenderer_amd.renderer import Renderer
+r = Renderer({scene_dir['full']!r}, device=0)
+for t in poses.script('P_over'):
+    r.update_and_render({w}, {h}, t)
+dist.init_process_group('nccl', init_method='tcp://127.0.0.1:{free_port()}', rank=0, world_size=1)
+try:
+    bg = BandGather({w}, {h}, 16, 1, 0, torch.device('cuda'))
+    r.render_bands(poses.hold('P_over'), {w}, {h}, 16, 1, 0, bg.send.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got = bg.gather()
+    torch.cuda.synchronize()
+    np.save({str(out)!r}, got.cpu().numpy().view(np.uint32))
+finally:
+    dist.destroy_process_group()
+    r.shutdown()
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get('PYTHONPATH', ''), MASTER_ADDR='127.0.0.1')
+    res = subprocess.run([sys.executable, '-c', code], cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert np.array_equal(np.load(out), want)
