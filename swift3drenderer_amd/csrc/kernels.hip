@@ -1607,7 +1607,11 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 #ifndef S3R_TSTAGE
 #define S3R_TSTAGE 128
 #endif
+#ifndef S3R_TSTAGE_LINK
+#define S3R_TSTAGE_LINK 256
+#endif
 constexpr uint32_t kTileW = 64, kTileH = 16, kTileThreads = 256, kTileStage = S3R_TSTAGE;
+constexpr uint32_t kTileStageLink = S3R_TSTAGE_LINK;     // the fused raster of delivered frames
 static_assert(kTileStage <= kTileThreads, "one staged triangle per thread at most");
 constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of one column hit different banks
 constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
@@ -2197,12 +2201,13 @@ __global__ void __launch_bounds__(256) k_tile_fill(const uint4 *__restrict__ liv
     }
 }
 
+template <uint32_t STAGE>
 struct TileShared {
     unsigned long long key[kTileH * kKeyStride];
-    float ws[3][kTileStage], dx[3][kTileStage], dy[3][kTileStage], rz[3][kTileStage];
-    uint32_t slot[kTileStage], xmin[kTileStage], xmax[kTileStage], ymin[kTileStage], r0[kTileStage];
-    uint32_t pre[kTileStage + 1];
-    uint16_t item[kTileStage * kTileH];            // item -> staged triangle
+    float ws[3][STAGE], dx[3][STAGE], dy[3][STAGE], rz[3][STAGE];
+    uint32_t slot[STAGE], xmin[STAGE], xmax[STAGE], ymin[STAGE], r0[STAGE];
+    uint32_t pre[STAGE + 1];
+    uint16_t item[STAGE * kTileH];            // item -> staged triangle
     uint32_t wsum[kTileThreads / 64];
     uint32_t bstart[kDepthBuckets];                // the tile's list position where each depth bucket starts
     uint32_t zwave[kTileThreads / 64];             // per wave: min over its pixels of the winner's 1/z bits
@@ -2302,14 +2307,15 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
 // with frame_rows its frame row) -- no per-pixel key round trip through HBM and, for frames written
 // into the caller's buffer, each tile's stores cross the link while other tiles rasterize; pixels
 // whose winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).
-template <bool FUSED>
+template <bool FUSED, uint32_t STAGE = kTileStage>
 __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
     const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0,
     ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred,
     uint32_t *__restrict__ counts, uint32_t bin_cap, uint32_t xoff) {
-    __shared__ TileShared ls;
+    static_assert(STAGE <= kTileThreads, "one staged triangle per thread at most");
+    __shared__ TileShared<STAGE> ls;
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
     // set's next frame -- unless the list overflowed (the frame's fill runs again, render_api.cpp)
@@ -2357,12 +2363,12 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         n = *total > cap ? 0u : end - base;
         if (tid < kDepthBuckets) ls.bstart[tid] = offs[s0 + tid] - base;
     }
-    // software pipeline: stage c0 + kTileStage's list entries and records are loaded into registers
+    // software pipeline: stage c0 + STAGE's list entries and records are loaded into registers
     // while stage c0's items run
     uint32_t s_nx = 0;
     float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n, q3n = q0n;
     auto fetch = [&](uint32_t c) {
-        if (tid < kTileStage && c + tid < n) {
+        if (tid < STAGE && c + tid < n) {
             if (bin_cap) {
                 const uint32_t v = c + tid;
                 uint32_t b = 0;                                  // the bucket holding entry v
@@ -2393,7 +2399,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
 #ifdef S3R_STATS
     uint32_t st_staged = 0, st_culled = 0;
 #endif
-    for (uint32_t c0 = 0; c0 < n; c0 += kTileStage) {
+    for (uint32_t c0 = 0; c0 < n; c0 += STAGE) {
         __syncthreads();                                 // previous stage fully consumed
 #if !(defined(S3R_TNOHIZ) && S3R_TNOHIZ)
         // hierarchical depth: each tile row's farthest current winner (0 while a pixel has none)
@@ -2430,7 +2436,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
 #endif
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
-        if (tid < kTileStage && j < n) {
+        if (tid < STAGE && j < n) {
             const uint32_t s = s_nx;
             const float4 q0 = q0n, q1 = q1n, q2 = q2n, q3 = q3n;
             const uint32_t bx = f2u(q0.x), by = f2u(q0.y);
@@ -2463,7 +2469,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             ls.dy[0][tid] = q2.z; ls.dy[1][tid] = q2.w; ls.dy[2][tid] = q3.x;
             ls.rz[0][tid] = q3.y; ls.rz[1][tid] = q3.z; ls.rz[2][tid] = q3.w;
         }
-        fetch(c0 + kTileStage);
+        fetch(c0 + STAGE);
         // exclusive scan of the row counts over the stage (wave shuffles + wave totals)
         uint32_t inc = nr;
         for (uint32_t o = 1; o < 64u; o <<= 1) {
@@ -2474,11 +2480,11 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
         __syncthreads();
         uint32_t wbase = 0;
         for (uint32_t w = 0; w < wave; w++) wbase += ls.wsum[w];
-        if (tid < kTileStage) ls.pre[tid] = wbase + inc - nr;
+        if (tid < STAGE) ls.pre[tid] = wbase + inc - nr;
         uint32_t items = 0;
         for (uint32_t w = 0; w < kTileThreads / 64u; w++) items += ls.wsum[w];
 #if !(defined(S3R_TITEM) && S3R_TITEM)
-        if (tid < kTileStage)
+        if (tid < STAGE)
             for (uint32_t i = 0; i < nr; i++) ls.item[ls.pre[tid] + i] = (uint16_t)tid;
         __syncthreads();
 #endif
@@ -3125,10 +3131,19 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
     const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
-    hipLaunchKernelGGL(k_tile_raster<true>, dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W, band,
-                       nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), 0u, sc, out, frame_rows ? 1u : 0u, deferred,
-                       counts, bin_cap, xoff);
+    // frames written into the caller's buffer stage 256 triangles at a time, frames into HBM 128: on
+    // the stress scene (one MI355X, profiles/r04_tstage_ab.txt) the wider stage delivers 772 / 726 ->
+    // 802 / 803 fps (the raster waits on the link anyway, and half the stage rounds and barriers
+    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy)
+    const uint32_t capw = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
+    if (frame_rows)
+        hipLaunchKernelGGL((k_tile_raster<true, kTileStageLink>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+                           (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list,
+                           (unsigned long long *)nullptr, capw, 0u, sc, out, 1u, deferred, counts, bin_cap, xoff);
+    else
+        hipLaunchKernelGGL((k_tile_raster<true>), dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
+                           band, nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr, capw, 0u, sc,
+                           out, 0u, deferred, counts, bin_cap, xoff);
     hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred, ctr, out,
                        bin_cap ? 1u : 0u, sum_host);
 }
