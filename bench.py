@@ -125,13 +125,14 @@ def frame_roofline(W, H, nv, ni, na, ntex, textured, device_s, delivered_s):
     return out
 
 
-def load_traffic(workload_key):
-    """HBM bytes per fragment launch from the committed rocprofv3 --pmc summary (profiles/)."""
+def load_traffic(workload_key, field='hbm_bytes_per_launch'):
+    """HBM bytes per launch (the fragment kernel's, or with field='setup_hbm_bytes_per_launch' the
+    tile path's setup) from the committed rocprofv3 --pmc summary (profiles/pmc_traffic.json)."""
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(workload_key, {}).get('hbm_bytes_per_launch')
+        return d.get(workload_key, {}).get(field)
     except Exception:
         return None
 
@@ -414,6 +415,7 @@ def run_rank0(a, N, np, torch):
         # events on its stream from the frame's first launch to the stage's end, same frames as roofline
         'setup_ms': round(geo_ms / max(nfr, 1), 5),
         'setup_bytes_per_frame': (16 * nv + 4 * ni + 4 * pairs) if path == 2 else None,
+        'setup_traffic': load_traffic(workload, 'setup_hbm_bytes_per_launch') if path == 2 else None,
         'setup_bytes_note': ('tile path, a lower bound: vertices 16 B and indices 4 B read, a 4-B bin entry '
                              'written per binned entry; the 64-B raster record of each live slot is not counted '
                              '(bins mode does not count live slots)') if path == 2 else None,
