@@ -146,7 +146,8 @@ void s3r_host_stats(uint64_t out[12]);
  *             the GPU(s) whenever the threads finish after the devices (S3R_FILL_GPU=0..8 fixes the
  *             share in eighths);
  *   0 auto    (default) host fill; -1: S3R_DELIVERY (copy|direct|fill|auto) or auto.
- * Tile-path frames and buffers that cannot be page-locked are always copied.  fill_threads -1:
+ * Tile-path frames take copy or direct (auto: direct; host fill is a row-path delivery); buffers
+ * that cannot be page-locked are always copied.  fill_threads -1:
  * S3R_FILL_THREADS, or 4 (one device) / 8 (several).  Returns 0, or -1 on a bad mode or thread
  * count (0 or > 64).  s3r_delivery() returns the mode in effect (0-3). */
 int s3r_set_delivery(int mode, int fill_threads);
@@ -158,7 +159,7 @@ int s3r_set_delivery(int mode, int fill_threads);
  * the NUMA node of the buffer they were placed for (int64, -1 unknown); for fill thread t = 1..n at
  * out[8 + 4(t - 1)]: the CPU it last ran on,
  * its summed finish time, the background pixels it wrote, its summed time in covered bins (their
- * background chunks, and the widening of staged chunks under the packed delivery).  Returns n
+ * background chunks).  Returns n
  * (<= max_threads); out holds 8 + 4 * max_threads words. */
 uint32_t s3r_fill_profile(uint64_t *out, uint32_t max_threads);
 int s3r_delivery(void);

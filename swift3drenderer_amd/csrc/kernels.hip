@@ -21,6 +21,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <rocprim/device/device_scan.hpp>
@@ -889,89 +891,6 @@ S3R_CALLEE uint32_t shade_core_flat(float4 c0, float4 c1, float4 c2, float4 n0, 
     return res;
 }
 
-#ifndef S3R_SHADE_PK
-#define S3R_SHADE_PK 0
-#endif
-// shade_core_flat with the independent f32 chains paired into v_pk_{mul,add,fma}_f32 (two lanes per
-// instruction; the same IEEE operations, so the same bits): the quotients w0, w1 / (1/z), the texture
-// coordinates (u, v) and their level quotients, the position and normal interpolations and their
-// normalisations side by side (P in the low halves, N in the high), the colour's (r, g).  For the
-// waterfall shading, whose constants sit in SGPRs: each packed source is an SGPR pair or a broadcast.
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v pfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2v pdiv_recip(f2v b) {
-    const f2v r = {S3R_RCP(b.x), S3R_RCP(b.y)};
-    return pfma(pfma(-b, r, (f2v){1.0f, 1.0f}), r, r);
-}
-__device__ __forceinline__ f2v pdiv_with_recip(f2v a, f2v b, f2v r) {
-    const f2v q0 = a * r;
-    const f2v q1 = pfma(pfma(-b, q0, a), r, q0);
-    return pfma(pfma(-b, q1, a), r, q1);
-}
-__device__ __forceinline__ f2v psqrt_in_range(f2v x) {
-    const f2v s = {S3R_SQRT(x.x), S3R_SQRT(x.y)};
-    const u2v su = __builtin_bit_cast(u2v, s);
-    const f2v sm = __builtin_bit_cast(f2v, su - 1u), sp = __builtin_bit_cast(f2v, su + 1u);
-    const f2v rm = pfma(-sm, s, x), rp = pfma(-sp, s, x);
-    const float tx = rm.x <= 0.0f ? sm.x : s.x, ty = rm.y <= 0.0f ? sm.y : s.y;
-    return (f2v){rp.x > 0.0f ? sp.x : tx, rp.y > 0.0f ? sp.y : ty};
-}
-S3R_CALLEE uint32_t shade_core_pk(float4 c0, float4 c1, float4 c2, float4 n0, float4 n1, float4 n2, float4 k0,
-                                  float4 k1, float4 k2, uint32_t kind, uint32_t tex_base, float w0, float w1,
-                                  float w2, float ooz, const uint32_t *__restrict__ tex, uint32_t ntex) {
-    auto inr = [](float x) { return (fabsf(x) >= 0x1p-40f) & (fabsf(x) < 0x1p20f); };
-    bool ok = inr(w0) & inr(w1) & inr(w2) & inr(ooz);
-    const float r = div_recip(ooz);
-    const f2v oo = {ooz, ooz}, rr = {r, r};
-    const f2v ab = pdiv_with_recip((f2v){w0, w1}, oo, rr);
-    const float a = ab.x, b = ab.y, c = div_with_recip(w2, ooz, r);
-    // texture coordinates first: the texel load overlaps the normalisations
-    const f2v muv = ((f2v){k0.x, k0.y} * a + (f2v){k0.z, k0.w} * b) + (f2v){k1.x, k1.y} * c;
-    const f2v dvv = (f2v){k2.x, k2.y} - muv * (f2v){k1.z, k1.w};
-    const f2v dv = {fabsf(dvv.x), fabsf(dvv.y)};
-    const bool texd = kind != kColour;
-    ok &= !texd | (inr(dv.x) & inr(dv.y));
-    const f2v lv = pdiv_with_recip(oo, dv, pdiv_recip(dv));
-    const bool tex_ok = texd & (tex_base < ntex) & (ntex - tex_base >= kTexTexels);
-    uint32_t rgb = tex[tex_ok ? tex_base + texel_offset(muv.x, muv.y, lv.x, lv.y) : 0u];
-    // (P, N) side by side: X = (P.x, N.x), ...
-    const f2v X = ((f2v){c0.x, n0.x} * a + (f2v){c1.x, n1.x} * b) + (f2v){c2.x, n2.x} * c;
-    const f2v Y = ((f2v){c0.y, n0.y} * a + (f2v){c1.y, n1.y} * b) + (f2v){c2.y, n2.y} * c;
-    const f2v Z = ((f2v){c0.z, n0.z} * a + (f2v){c1.z, n1.z} * b) + (f2v){c2.z, n2.z} * c;
-    const f2v d = (X * X + Y * Y) + Z * Z;                                            // simd_dot
-    ok &= sqrt_in_range_ok(d.x) & sqrt_in_range_ok(d.y);
-    const f2v sq = psqrt_in_range(d);
-    const f2v inv = pdiv_with_recip((f2v){1.0f, 1.0f}, sq, pdiv_recip(sq));
-    const f2v nx = X * inv, ny = Y * inv, nz = Z * inv;           // (pn, normal) components
-    // halfway = normalize(-pn + normal); s = dot(halfway, normal)
-    const F3 h = mk3(-nx.x + nx.y, -ny.x + ny.y, -nz.x + nz.y);
-    const float hd = dot3(h, h);
-    ok &= sqrt_in_range_ok(hd);
-    const float hs = sqrt_in_range(hd);
-    const float hinv = div_with_recip(1.0f, hs, div_recip(hs));
-    const F3 hw = mk3(h.x * hinv, h.y * hinv, h.z * hinv);
-    float s = dot3(hw, mk3(nx.y, ny.y, nz.y));
-    asm volatile("" : "+v"(rgb), "+v"(s));
-    rgb = tex_ok ? rgb : 0u;
-    f2v cxy;
-    float cz;
-    if (texd) {
-        cxy = (f2v){(float)(rgb >> 16), (float)((rgb >> 8) & 255u)};
-        cz = (float)(rgb & 255u);
-    } else {
-        cxy = ((f2v){k0.x, k0.y} * a + (f2v){k1.x, k1.y} * b) + (f2v){k2.x, k2.y} * c;
-        cz = (k0.z * a + k1.z * b) + k2.z * c;
-    }
-    const f2v sc = cxy * s;
-    uint32_t res = rgb_pack(sc.x, sc.y, s * cz);
-    if (!ok) {
-        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(ooz));
-        res = shade_core<false>(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, w0, w1, w2, ooz, tex, ntex);
-    }
-    return res;
-}
-
 // The same from a TriSetup record (tile path: a register-resident record).
 S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, float w2, float ooz,
                           const uint32_t *__restrict__ tex, uint32_t ntex) {
@@ -1145,8 +1064,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                                   const uint4 *__restrict__ pairs, uint32_t *done_flag,
                                                   uint32_t prev_tag, uint32_t *__restrict__ order,
                                                   uint32_t host_fill, unsigned long long *chunk_flags,
-                                                  uint32_t fill_tag, uint32_t row_starts,
-                                                  uint8_t *__restrict__ pstage) {
+                                                  uint32_t fill_tag, uint32_t row_starts) {
     __shared__ FragShared sh;
     S3R_WGT(0);
     // Completion for the host (buffer-set reuse without events, render_api.cpp wait_set_free): this
@@ -1301,26 +1219,6 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         const uint32_t o = lane >= rsh ? rot : carry;
         if (o != kNoPixel) row[c0x - rsh + lane] = o;
         carry = rot;
-    };
-    // HOSTW with pstage (packed delivery, render_api.cpp): a whole covered chunk goes over the link
-    // at 3 bytes a pixel into the staging frame -- bin-major: bin b's rows x segment pixels at
-    // pstage + b x (kWaves x segment x 3), its row (wave) w at + w x segment x 3 -- 192 bytes, lanes
-    // 0..47 one dword each, gathered from the lanes of its pixels; the host widens it into the
-    // caller's buffer once the bin's chunk mask is in; a chunk cut by the frame's right edge is
-    // stored directly.  The link carries 3/4 of the covered pixels' bytes.
-    constexpr uint32_t kSegStage = 3u * kChunk * SEGCH;
-    uint8_t *const srow = (HOSTW && pstage) ? pstage + (size_t)bid * (kWaves * kSegStage) + wave * kSegStage : nullptr;
-    auto put_packed = [&](uint32_t c0x, uint32_t v) {
-        const uint32_t b = 4u * lane, i0 = b / 3u, o = b - 3u * i0;
-        const uint32_t a0 = (uint32_t)__shfl((int)v, (int)min(i0, 63u));
-        const uint32_t a1 = (uint32_t)__shfl((int)v, (int)min(i0 + 1u, 63u));
-        const uint32_t w = o == 0u ? (a0 & 0xFFFFFFu) | (a1 << 24) : o == 1u ? ((a0 >> 8) & 0xFFFFu) | (a1 << 16)
-                                                                          : ((a0 >> 16) & 0xFFu) | (a1 << 8);
-        // system-scope stores: their completion (the s_waitcnt before the chunk mask) is their arrival
-        // in host memory, so the host never reads a staged chunk before its bytes
-        if (lane < 48u)
-            __hip_atomic_store(reinterpret_cast<uint32_t *>(srow + 3u * (c0x - xs)) + lane, w, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
     };
     S3R_WGC_DECL;
     for (uint32_t q = 0; q < SEGCH; q++) {
@@ -1498,16 +1396,11 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 #if defined(S3R_ABLATE) && (S3R_ABLATE & 512)     // ablation: every shade reads one record
                 row[xp] = win[p] < 0 ? kBackground : shade(tris + 40, bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
 #else
-            // (packed: a whole chunk of a valid row; kPX == 1, row_ok is wave-uniform)
-            const bool packed = HOSTW && kPX == 1u && srow != nullptr && row_ok && cx0 + kChunk - 1u <= xe;
             if (!WF) {
                 const bool act = row_ok && xp <= xe;
                 uint32_t px = kNoPixel;
                 if (act) px = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
-                if (packed) {
-                    put_packed(cx0, px);
-                    put(cx0 + 64u * p, kNoPixel);
-                } else if (HOSTW) {
+                if (HOSTW) {
                     put(cx0 + 64u * p, px);
                 } else if (act) {
                     row[xp] = px;
@@ -1532,18 +1425,10 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                     const bool mine = act && wp == wu;
                     todo &= ~__ballot(mine);
                     if (mine)
-#if S3R_SHADE_PK
-                        px = shade_core_pk(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
-                                           depth[p], tex, ntex);
-#else
                         px = shade_core_flat(c0, c1, c2, n0, n1, n2, k0, k1, k2, kind, tex_base, bw0[p], bw1[p], bw2[p],
                                              depth[p], tex, ntex);
-#endif
                 }
-                if (packed) {
-                    put_packed(cx0, px);
-                    put(cx0 + 64u * p, kNoPixel);
-                } else if (HOSTW) {
+                if (HOSTW) {
                     put(cx0 + 64u * p, act ? px : kNoPixel);
                 } else if (act) {
                     row[xp] = px;
@@ -1556,10 +1441,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     }
     if (HOSTW && rsh != 0u && lane < rsh && carry != kNoPixel) row[cx_next - rsh + lane] = carry;
     if (HOSTW && host_fill) {
-        // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q).  With staged
-        // chunks, every wave's stores are complete before the mask is stored after them: the host
-        // reads the staging frame once it sees the mask (both cross the link in that order)
-        if (pstage) __builtin_amdgcn_s_waitcnt(0);
+        // this bin's background chunks for the host: (tag << 32) | bit (wave * SEGCH + q)
         if (lane == 0) sh.bgm[wave] = bgm;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2303,15 +2185,17 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
     return shade(&ts, w0, w1, w2, ooz, sc.tex, sc.ntex);
 }
 
-// FUSED: the tile's winners are shaded here, straight from LDS, and stored to out (its local row, or
-// with frame_rows its frame row) -- no per-pixel key round trip through HBM and, for frames written
-// into the caller's buffer, each tile's stores cross the link while other tiles rasterize; pixels
-// whose winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).
-template <bool FUSED, uint32_t STAGE = kTileStage>
+// The tile's winners are shaded here, straight from LDS, and stored to out (its local row, or with
+// frame_rows its frame row) -- no per-pixel key round trip through HBM and, for frames written into
+// the caller's buffer, each tile's stores cross the link while other tiles rasterize; pixels whose
+// winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).  (Round 4 measured
+// the split form -- keys through HBM, a per-pixel resolve launch -- slower everywhere: stress scene
+// whole frame 800 -> 854 fps fused, delivered 583 -> 614, part 0 of 8 4 491 -> 4 672; it is gone.)
+template <uint32_t STAGE = kTileStage>
 __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
-    const uint32_t *__restrict__ list, unsigned long long *__restrict__ keys, uint32_t cap, uint32_t tile0,
+    const uint32_t *__restrict__ list, uint32_t cap,
     ShadeScene sc, uint32_t *__restrict__ out, uint32_t frame_rows, uint4 *__restrict__ deferred,
     uint32_t *__restrict__ counts, uint32_t bin_cap, uint32_t xoff) {
     static_assert(STAGE <= kTileThreads, "one staged triangle per thread at most");
@@ -2319,10 +2203,10 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     const uint32_t *const total = ctr + 1;
     // the fill (complete before this launch) was the live counters' last reader: reset them for the
     // set's next frame -- unless the list overflowed (the frame's fill runs again, render_api.cpp)
-    if (!bin_cap && tile0 == 0u && blockIdx.x == 0u && threadIdx.x < kTileShards && *total <= cap)
+    if (!bin_cap && blockIdx.x == 0u && threadIdx.x < kTileShards && *total <= cap)
         *shard_ctr(ctr, 1, threadIdx.x) = 0u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t tile = tile0 + blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const uint32_t tile = blockIdx.x, ty = tile / tiles_x, tx = tile - ty * tiles_x;
     // the tile's pixel columns: [64 tx - xoff, 64 tx - xoff + 64) inside the frame (tile_box)
     const uint32_t lx0 = max(tx * kTileW, xoff) - xoff, lx1 = min(W, tx * kTileW + kTileW - xoff) - 1u;
     const uint32_t tr0 = ty * kTileH, tr1 = min(rows_local, tr0 + kTileH) - 1u;
@@ -2372,6 +2256,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
             if (bin_cap) {
                 const uint32_t v = c + tid;
                 uint32_t b = 0;                                  // the bucket holding entry v
+                static_assert(kDepthBuckets == 32, "the bucket search covers 32 buckets");
 #pragma unroll
                 for (uint32_t step = 16; step >= 1u; step >>= 1)
                     if (ls.bstart[b + step] <= v) b += step;
@@ -2566,7 +2451,7 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
     }
 #endif
     __syncthreads();
-    if (FUSED) {
+    {
         for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {   // (wave-uniform trip count)
             const uint32_t rr = i / kTileW, cc = i % kTileW;
             const uint32_t lr = tr0 + rr, x = lx0 + cc;
@@ -2587,12 +2472,6 @@ __global__ void __launch_bounds__(kTileThreads) k_tile_raster(
                         deferred, ctr + 3);
             if (in && v != kDeferPixel) out[idx] = v;
         }
-        return;
-    }
-    for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {
-        const uint32_t rr = i / kTileW, cc = i % kTileW;
-        const uint32_t lr = tr0 + rr, x = lx0 + cc;
-        if (lr <= tr1 && x <= lx1) keys[(size_t)lr * W + x] = ls.key[rr * kKeyStride + cc];
     }
 }
 
@@ -2627,37 +2506,6 @@ __global__ void __launch_bounds__(256) k_tile_resolve_deferred(ShadeScene sc, co
 #endif
         out[e.x] = resolve_pixel<false>(sc, k, e.w & 0xFFFFu, e.w >> 16);
     }
-}
-
-// One thread per pixel: the winner of each pixel (key), re-walked exactly from its raster record
-// and shaded with constants recomputed from the scene (resolve_pixel); background where no fragment;
-// a pixel whose winner needs its full setup (clip) is queued for k_tile_resolve_deferred.
-__global__ void __launch_bounds__(256) k_tile_resolve(
-    const unsigned long long *__restrict__ keys, const RasterRec *__restrict__ recs, const float4 *__restrict__ vtx,
-    const float4 *__restrict__ nrm, const float4 *__restrict__ pay, const uint8_t *__restrict__ disc,
-    const uint32_t *__restrict__ vidx, const uint32_t *__restrict__ aidx, uint32_t ntri, Mat34 m, float factor,
-    float sw, float sh, const uint32_t *__restrict__ tex, uint32_t ntex, uint32_t *__restrict__ out, uint32_t W,
-    uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local, uint32_t frame_rows, uint32_t by0,
-    uint4 *__restrict__ deferred, uint32_t *__restrict__ ctr) {
-    const uint32_t lr = (by0 + blockIdx.y) * 4u + (threadIdx.x >> 6);
-    if (lr >= rows_local) return;
-    const uint32_t y = nparts == 1u ? lr : ((lr / band) * nparts + part) * band + lr % band;
-    // frame_rows == 2 (the caller's mapped frame, uncached registration): each wave's 64 pixels start
-    // on the 64-B line grid of the caller's row -- a row of a malloc'd buffer begins rsh pixels into a
-    // line, so the wave takes pixels [64 bx - rsh, 64 bx - rsh + 64) (one block more per row) and its
-    // store crosses the link as four whole lines instead of five partly written ones
-    uint32_t x = blockIdx.x * 64u + (threadIdx.x & 63u);
-    if (frame_rows == 2u) x -= (uint32_t)(((uintptr_t)(out + (size_t)y * W)) >> 2) & 15u;
-    const bool in = x < W;                             // (x wrapped below 0 included)
-    const size_t idx = (size_t)lr * W + x;
-    const ShadeScene sc{recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
-    const unsigned long long k = in ? keys[idx] : 0ull;
-    const uint32_t v = in ? resolve_pixel<true>(sc, k, x, y) : kBackground;
-    const size_t o = frame_rows ? (size_t)y * W + x : idx;   // (frame_rows: the caller's mapped frame)
-    // a winner that needs its full setup: the pixel goes to k_tile_resolve_deferred
-    wave_append(in && v == kDeferPixel, make_uint4((uint32_t)o, (uint32_t)k, (uint32_t)(k >> 32), (x & 0xFFFFu) | (y << 16)),
-                deferred, ctr + 3);
-    if (in && v != kDeferPixel) out[o] = v;
 }
 
 // ------------------------------------------------------------------ self-test kernel
@@ -2788,6 +2636,34 @@ void stats_read(unsigned long long out[24], bool reset) {
 }
 
 // ------------------------------------------------------------------ launchers
+// S3R_CHECK=1: each launch synchronised and checked (s3r_kernels.h).  The context is per host
+// thread: with several devices behind updateAndRender each device's worker launches its own part.
+static thread_local int t_check_dev = -1;
+static thread_local uint32_t t_check_frame = 0;
+static thread_local const char *t_check_stage = "";
+
+bool check_launches() {
+    static const bool on = getenv("S3R_CHECK") && atoi(getenv("S3R_CHECK")) != 0;
+    return on;
+}
+
+void check_context(int device, uint32_t frame, const char *stage) {
+    t_check_dev = device;
+    t_check_frame = frame;
+    t_check_stage = stage;
+}
+
+void after_launch(const char *kernel, hipStream_t st) {
+    if (!check_launches()) return;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        fprintf(stderr, "s3r: S3R_CHECK: %s after %s (device %d, frame %u, %s)\n", hipGetErrorName(e), kernel,
+                t_check_dev, t_check_frame, t_check_stage);
+        abort();
+    }
+}
+
 #ifndef S3R_SEG_PIXELS
 #define S3R_SEG_PIXELS 384
 #endif
@@ -2852,11 +2728,11 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
         // nothing to set up (every bin is sky), or more row blocks than counters: k_sky_flags publishes
         if (ntri && rows_local) {
             const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-            hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
+            { hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
                                   st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
                                   nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
                                   (uint32_t)fragment_bins(W, rows_local), order, nrb,
-                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u);
+                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u); after_launch("k_geometry", st); }
         }
         if (gsf)
             launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
@@ -2870,10 +2746,10 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
+    { hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u);
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u); after_launch("k_geometry", st); }
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
@@ -2881,7 +2757,7 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
                      bool frame_rows, uint32_t host_fill, unsigned long long *chunk_flags, uint32_t fill_tag,
-                     bool row_starts, uint8_t *stage) {
+                     bool row_starts) {
     const uint32_t segs = fragment_segments(W);
     const uint64_t blocks = fragment_bins(W, rows_local);
     if (blocks == 0) {                                   // (render_core never asks for an empty frame part)
@@ -2897,13 +2773,13 @@ void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab,
     };
     auto kern = frame_rows ? pick(std::true_type{}) : pick(std::false_type{});
     if (done)
-        hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
+        { hipExtLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, nullptr, done, 0, tris, nslots,
                               rowtab, tex, ntex, out, W, H, band, nparts, part, segs, rows_local, bincnt, pairs,
-                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u, stage);
+                              done_flag, prev_tag, order, host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u); after_launch("k_fragment", st); }
     else
-        hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
+        { hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(64 * kWaves), 0, st, tris, nslots, rowtab, tex, ntex, out,
                            W, H, band, nparts, part, segs, rows_local, bincnt, pairs, done_flag, prev_tag, order,
-                           host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u, stage);
+                           host_fill, chunk_flags, fill_tag, row_starts ? 1u : 0u); after_launch("k_fragment", st); }
 }
 
 // Host fill (render_api.cpp): once k_geometry's pair counts are final, one flag per fragment bin in
@@ -2933,8 +2809,8 @@ void launch_sky_flags(const uint32_t *bincnt, uint64_t nbins, uint32_t *flags, u
         if (done) (void)hipEventRecord(done, st);
         return;
     }
-    hipExtLaunchKernelGGL(k_sky_flags, dim3(blocks), dim3(256), 0, st, nullptr, done, 0, bincnt, (uint32_t)nbins, flags,
-                          tag, probe, gpu_eighths);
+    { hipExtLaunchKernelGGL(k_sky_flags, dim3(blocks), dim3(256), 0, st, nullptr, done, 0, bincnt, (uint32_t)nbins, flags,
+                          tag, probe, gpu_eighths); after_launch("k_sky_flags", st); }
 }
 
 // ------------------------------------------------------------------ band de-interleave
@@ -2965,11 +2841,11 @@ void launch_deinterleave_bands(const uint32_t *gathered, uint32_t part_stride_ro
     const dim3 grid((W + 1023u) / 1024u, H);
     const bool v4 = W % 4 == 0 && ((uintptr_t)gathered & 15u) == 0 && ((uintptr_t)frame & 15u) == 0;
     if (v4)
-        hipLaunchKernelGGL(k_deinterleave_bands<true>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band, nparts,
-                           frame);
+        { hipLaunchKernelGGL(k_deinterleave_bands<true>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band, nparts,
+                           frame); after_launch("k_deinterleave_bands", st); }
     else
-        hipLaunchKernelGGL(k_deinterleave_bands<false>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band,
-                           nparts, frame);
+        { hipLaunchKernelGGL(k_deinterleave_bands<false>, grid, dim3(256), 0, st, gathered, part_stride_rows, W, band,
+                           nparts, frame); after_launch("k_deinterleave_bands", st); }
 }
 
 // Test hook (include/render.h s3r_ooz_bound): the tile path's 1/z bound of a raster setup, computed
@@ -3045,13 +2921,13 @@ void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const 
                   void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
                   hipStream_t st, uint32_t *tbin, uint32_t bin_cap) {
     const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
-    hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
+    { hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
                        0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, xoff,
-                       (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap);
+                       (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap); after_launch("k_tile_setup", st); }
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
-    hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
+    { hipLaunchKernelGGL((k_tile_clip<CL>), dim3(kTileShards), dim3(256), 0, st, vtx, vidx, ntri, cmap, perm, tab, m,
                        factor, sw, sh, band, nparts, part, tx, xoff, (RasterRec *)recs, live, clipq, ctr, counts, tbin,
-                       bin_cap);
+                       bin_cap); after_launch("k_tile_clip", st); }
 }
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
@@ -3063,12 +2939,12 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
     const uint64_t ns = tile_slots(W, rows_local, xoff);  // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
-        hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv);
+        { hipLaunchKernelGGL(k_tile_vertex, dim3((nv + 255) / 256), dim3(256), 0, st, vtx, nv, m, factor, sw / 2, sh / 2, vrv); after_launch("k_tile_vertex", st); }
     if (ntri) {
         const uint32_t tx = tile_grid_x(W, xoff);
         if (clustered) {
-            hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
-                               cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr);
+            { hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
+                               cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr); after_launch("k_cluster_cull", st); }
             setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
                                       ctr, counts, nullptr, st, tbin, bin_cap);
         } else if (vrv) {
@@ -3080,45 +2956,32 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
         }
     }
     if (bin_cap) {                                       // bins mode: binned already
-        hipLaunchKernelGGL(k_tile_bins_done, dim3(1), dim3(64), 0, st, ctr, sum_host, tag);
+        { hipLaunchKernelGGL(k_tile_bins_done, dim3(1), dim3(64), 0, st, ctr, sum_host, tag); after_launch("k_tile_bins_done", st); }
         return;
     }
     size_t bytes = scan_temp_bytes;
     (void)rocprim::exclusive_scan(scan_temp, bytes, (const uint32_t *)counts, offs, 0u, (size_t)ns,
                                   rocprim::plus<uint32_t>(), st);
-    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
-                       cursor, ctr, 1u, sum_host, tag);
+    after_launch("rocprim_exclusive_scan", st);
+    { hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, counts, offs, (uint32_t)ns,
+                       cursor, ctr, 1u, sum_host, tag); after_launch("k_tile_cursor", st); }
 }
 
 void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W, uint32_t rows_local, uint32_t *cursor,
                         uint32_t *ctr, hipStream_t st, uint32_t xoff) {
     const uint64_t ns = tile_slots(W, rows_local, xoff);
     if (ns == 0) return;
-    hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, (uint32_t *)counts, offs,
-                       (uint32_t)ns, cursor, ctr, 0u, (uint32_t *)nullptr, 0u);
+    { hipLaunchKernelGGL(k_tile_cursor, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, st, (uint32_t *)counts, offs,
+                       (uint32_t)ns, cursor, ctr, 0u, (uint32_t *)nullptr, 0u); after_launch("k_tile_cursor", st); }
 }
 
 void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
                       uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
                       hipStream_t st, uint32_t xoff) {
     if (ntri == 0) return;
-    hipLaunchKernelGGL(k_tile_fill, dim3(shard_grid(k_tile_fill, ntri)), dim3(256), 0, st, live, ctr,
+    { hipLaunchKernelGGL(k_tile_fill, dim3(shard_grid(k_tile_fill, ntri)), dim3(256), 0, st, live, ctr,
                        cl && cl->ncl ? cl->shard : nullptr, ntri, band, nparts, part, tile_grid_x(W, xoff), cursor, list,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull));
-}
-
-void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                        uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
-                        unsigned long long *keys, uint64_t cap, hipStream_t st, uint32_t ty0, uint32_t ty1,
-                        uint32_t *counts, uint32_t bin_cap, uint32_t xoff) {
-    const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
-    ty1 = std::min(ty1, ty);            // (HIP's host min() is int: 0xFFFFFFFF would read as -1)
-    if (tx == 0 || ty0 >= ty1) return;
-    const ShadeScene none{};
-    hipLaunchKernelGGL(k_tile_raster<false>, dim3(tx * (ty1 - ty0)), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
-                       band, nparts, part, rows_local, tx, offs, ctr, list, keys,
-                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull), ty0 * tx, none, (uint32_t *)nullptr, 0u,
-                       (uint4 *)nullptr, counts, bin_cap, xoff);
+                       (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull)); after_launch("k_tile_fill", st); }
 }
 
 void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
@@ -3137,29 +3000,15 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
     // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy)
     const uint32_t capw = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
     if (frame_rows)
-        hipLaunchKernelGGL((k_tile_raster<true, kTileStageLink>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+        { hipLaunchKernelGGL((k_tile_raster<kTileStageLink>), dim3(tx * ty), dim3(kTileThreads), 0, st,
                            (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list,
-                           (unsigned long long *)nullptr, capw, 0u, sc, out, 1u, deferred, counts, bin_cap, xoff);
+                           capw, sc, out, 1u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
     else
-        hipLaunchKernelGGL((k_tile_raster<true>), dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
-                           band, nparts, part, rows_local, tx, offs, ctr, list, (unsigned long long *)nullptr, capw, 0u, sc,
-                           out, 0u, deferred, counts, bin_cap, xoff);
-    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred, ctr, out,
-                       bin_cap ? 1u : 0u, sum_host);
-}
-
-void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
-                         const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
-                         uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
-                         uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows, uint32_t r0, uint32_t r1,
-                         bool line_grid, uint4 *deferred, uint32_t *ctr) {
-    r1 = std::min(r1, rows_local);
-    if (W == 0 || r0 >= r1 || (r0 & 3u)) return;
-    const uint32_t mode = frame_rows ? (line_grid ? 2u : 1u) : 0u;
-    hipLaunchKernelGGL(k_tile_resolve, dim3((W + 63) / 64 + (mode == 2u ? 1u : 0u), (r1 - r0 + 3) / 4), dim3(256), 0,
-                       st, keys, (const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, sw, sh, tex,
-                       ntex, out, W, band, nparts, part, r1, mode, r0 / 4u, deferred, ctr);
+        { hipLaunchKernelGGL((k_tile_raster<>), dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
+                           band, nparts, part, rows_local, tx, offs, ctr, list, capw, sc,
+                           out, 0u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
+    { hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred, ctr, out,
+                       bin_cap ? 1u : 0u, sum_host); after_launch("k_tile_resolve_deferred", st); }
 }
 
 void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
@@ -3168,8 +3017,8 @@ void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const flo
                                   uint32_t *out, const uint4 *deferred, uint32_t *ctr, hipStream_t st, bool bins,
                                   uint32_t *sum_host) {
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
-    hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, deferred, ctr, out, bins ? 1u : 0u,
-                       sum_host);
+    { hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, deferred, ctr, out, bins ? 1u : 0u,
+                       sum_host); after_launch("k_tile_resolve_deferred", st); }
 }
 
 }  // namespace s3r

@@ -46,7 +46,6 @@ void build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_
 }
 namespace s3r_host {   // host_fill.cpp
 void fill_words(uint32_t *p, size_t n, uint32_t v);
-void widen_pixels(const uint8_t *src, uint32_t *dst, size_t n);
 void store_fence();
 }
 
@@ -78,8 +77,8 @@ constexpr uint64_t kLptMinBins = 2000;      // longest-first fragment order from
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
 // the order-independent tile path takes over (the icosahedron stress scene).
 constexpr uint64_t kRowPathMaxSlots = 8192;
-constexpr uint32_t kDefaultBand = 16;
-constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set       // rows per interleaved band when updateAndRender spans devices
+constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
+constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set
 constexpr int kMaxDevices = 64;
 
 // S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
@@ -104,7 +103,6 @@ struct HostProf {
 };
 
 // One GPU: its replica of the scene, its per-frame buffer sets, streams and frame tags.
-constexpr uint32_t kMaxTileSlabs = 16;
 
 struct Dev {
     int device = -1;
@@ -138,8 +136,6 @@ struct Dev {
     float4 *cl_sphere = nullptr;
     uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_shard = nullptr, *cl_map = nullptr;
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
-    unsigned long long *keys = nullptr;        // W x rows per-pixel (1/z, slot) winners
-    size_t keys_cap = 0;
     uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
     size_t deferred_cap = 0;
     // bins (the default; S3R_TILE_BINS=0: the lists): per buffer set, bin_cap entries for every (tile, bucket) slot
@@ -160,14 +156,11 @@ struct Dev {
     bool tile_frame_rows = false;
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
+    int last_set = -1;                         // tile path: the last frame's buffer set (refresh_pairs)
+    bool last_set_bins = false;                // ... binned (its entry total arrives at the frame's end)
     uint64_t last_live = 0, last_kept = 0;     // tile path, last read-back frame: live slots, cluster-kept triangles
     int last_path = 0;                         // 1 rows, 2 tiles: the last frame's fragment stage
     hipEvent_t geo_done[kSets] = {}, frag_done[kSets] = {};
-    // tile path with direct delivery: the fragment stage in row slabs, slab k's resolve (its stores
-    // cross the link) on res_stream while slab k + 1 rasterizes on the frame's stream (created on
-    // first use)
-    hipStream_t res_stream = nullptr;
-    hipEvent_t slab_done[kMaxTileSlabs] = {}, res_done = nullptr;
     // row path, buffer-set reuse without events: each k_fragment launch stores the tag of the previous
     // fragment launch (complete by stream order) in *done_host (host-coherent memory; done_dev is its
     // device address); issued_tag[p] = the tag of the last fragment launch that read set p (0: none);
@@ -176,8 +169,6 @@ struct Dev {
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
     uint32_t *geo_cnt = nullptr;             // host fill: per buffer set, k_geometry's bin-phase count
-    uint8_t *stage_dev = nullptr;            // packed delivery: this device's address of Lib::stage
-    uint64_t stage_epoch = 0;
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
     // the previous frame's stream; NULL is a valid caller stream (the legacy default stream), so
     // whether a previous frame exists is its own flag
@@ -342,11 +333,9 @@ struct Lib {
     bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
     bool clusters_whole = false;               // ... also for whole frames (S3R_CLUSTERS=2)
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
-    uint32_t tile_slabs = 1;                   // tile path, direct delivery: row slabs (S3R_TILE_SLABS)
-    bool tile_line_grid = true;                // tile path, direct delivery: line-grid wave stores (S3R_TILE_LINE)
+    bool tile_line_grid = true;                // tile path, direct delivery: tiles on the caller's line grid (S3R_TILE_LINE)
     bool tile_bins = true;                     // tile path: fixed-capacity bins filled by the setup (S3R_TILE_BINS)
     uint64_t tile_bin_budget = 32ull << 30;    // bytes of bins per device, all buffer sets (S3R_TILE_BIN_BUDGET_MB)
-    bool tile_fused = true;                    // tile path: raster and resolve in one launch (S3R_TILE_FUSED=0: two)
     bool serial = false;                       // S3R_SERIAL: no geometry/fragment overlap (profiling)
     bool timing = false;
 
@@ -370,10 +359,6 @@ struct Lib {
     int fill_threads = -1;                     // host fill threads; -1: S3R_FILL_THREADS or the default
     Pool fill_pool;
     int fill_node = -2;                        // NUMA node the fill threads were placed for
-    uint8_t *stage = nullptr;                  // packed delivery: the staging frame (host, 3 B a pixel)
-    size_t stage_cap = 0;
-    uint64_t stage_epoch = 0;                  // bumped when the staging frame is reallocated
-    int pack = -1;                             // packed delivery: -1 unset (S3R_PACK, default on)
     bool fill_placed = false;                  // fill threads pinned one per CPU domain (fill_placement)
     uint64_t copy_frames = 0, direct_frames = 0, fill_frames = 0;
     // adaptive host fill: eighths of the sky bins the GPUs write themselves, and the smoothed
@@ -635,16 +620,12 @@ void initialize() {
     }
     g.serial = getenv("S3R_SERIAL") != nullptr;
     {
-        const char *e = getenv("S3R_TILE_SLABS");
-        g.tile_slabs = e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1u;
         const char *l = getenv("S3R_TILE_LINE");
         g.tile_line_grid = !(l && atoi(l) == 0);
         const char *tb = getenv("S3R_TILE_BINS");
         g.tile_bins = !(tb && atoi(tb) == 0);
         const char *bb = getenv("S3R_TILE_BIN_BUDGET_MB");
         if (bb && atoll(bb) > 0) g.tile_bin_budget = (uint64_t)atoll(bb) << 20;
-        const char *f = getenv("S3R_TILE_FUSED");
-        g.tile_fused = !(f && atoi(f) == 0);
     }
     for (int id : ids) {
         Dev *d = new Dev();
@@ -680,7 +661,7 @@ void unregister_all() {
 
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
-    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.keys, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
+    void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
                     d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -701,34 +682,29 @@ void dev_release(Dev &d) {
     }
     for (hipStream_t gs : d.geo)
         if (gs) (void)hipStreamDestroy(gs);
-    for (hipEvent_t e : d.slab_done)
-        if (e) (void)hipEventDestroy(e);
-    if (d.res_done) (void)hipEventDestroy(d.res_done);
-    if (d.res_stream) (void)hipStreamDestroy(d.res_stream);
     for (auto &t : d.tslots) {
         (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
     }
     if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
-void free_stage() {
-    if (!g.stage) return;
-    (void)hipHostUnregister(g.stage);
-    free(g.stage);
-    g.stage = nullptr;
-    g.stage_cap = 0;
-}
-
 void release_all() {
     g.pool.stop();
     g.fill_pool.stop();
     if (g.initialized) {
+        // a device fault of an earlier frame surfaces here at the latest: report it as such (the
+        // context is unusable after it) rather than in whatever HIP call comes next
         for (Dev *d : g.devs) {
-            (void)hipSetDevice(d->device);
-            (void)hipDeviceSynchronize();
+            hipError_t e = hipSetDevice(d->device);
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e != hipSuccess) {
+                fprintf(stderr, "s3r: HIP error %s on device %d while releasing the library: a fault of an "
+                        "earlier frame's kernels (run with S3R_CHECK=1 to name the launch)\n", hipGetErrorName(e),
+                        d->device);
+                abort();
+            }
         }
         unregister_all();
-        free_stage();
         for (Dev *d : g.devs) {
             dev_release(*d);
             delete d;
@@ -906,60 +882,20 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     follow_previous_frame(d, st);
     HIPCHECK(hipStreamWaitEvent(st, d.geo_done[p], 0));
     if (ts) HIPCHECK(hipEventRecord(ts->frag0, st));
-    // Direct delivery in row slabs (S3R_TILE_SLABS = k > 1; whole tile rows): slab i's resolve, whose
-    // stores cross the link, on res_stream after slab i's raster, overlapping slab i + 1's raster on
-    // st; st joins res_stream at the end (the next frame's raster overwrites the keys).  Measured on
-    // the 4K stress frame: 1 slab 552-554 fps, 2: 483, 4: 461-463, 8: 407 -- off by default.
-    const uint32_t th = tile_height(), tyn = (rows_local + th - 1) / th;
-    uint32_t slabs = frame_rows ? g.tile_slabs : 1u;
-    slabs = std::max(1u, std::min({slabs, tyn, kMaxTileSlabs}));
-    // fused raster + resolve -- stress scene, one MI355X: whole frame 800 -> 854 fps in HBM, delivered
-    // 583 -> 614 (lists, profiles/r04_tile_fused_ab.txt); part 0 of 8 4 328 -> 4 026 with the lists,
-    // but 4 491-4 632 -> 4 672-4 696 with the bins (profiles/r04_part8_ab.txt), so for every frame
-    const bool fused = g.tile_fused;
+    // raster and resolve fused (kernels.hip k_tile_raster) -- stress scene, one MI355X: whole frame 800
+    // -> 854 fps in HBM, delivered 583 -> 614 (profiles/r04_tile_fused_ab.txt), part 0 of 8 4 491-4 632
+    // -> 4 672-4 696 with the bins (profiles/r04_part8_ab.txt); the split launches are gone (round 5)
     const size_t npx = (size_t)W * rows_local;
-    if (d.deferred_cap < npx) {                // pixels whose winner needs its full setup (either way)
+    if (d.deferred_cap < npx) {                // pixels whose winner needs its full setup
         HIPCHECK(hipDeviceSynchronize());
         if (d.deferred) HIPCHECK(hipFree(d.deferred));
         d.deferred = dalloc<uint4>(npx);
         d.deferred_cap = npx;
     }
-    if (fused) {
-        launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                                   d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
-                                   list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff,
-                                   d.tile_sum_dev + kSumWords * p);
-    } else if (slabs == 1u) {
-        launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list, d.keys,
-                           d.tile_list_cap[p], st, 0, 0xFFFFFFFFu, bcounts, bcap, d.tile_xoff);
-        launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw,
-                            sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, st, frame_rows, 0, 0xFFFFFFFFu,
-                            g.tile_line_grid, d.deferred, d.tile_ctr[p]);
-        launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], st, bins, d.tile_sum_dev + kSumWords * p);
-    } else {
-        if (!d.res_stream) {
-            HIPCHECK(hipSetDevice(d.device));
-            HIPCHECK(hipStreamCreateWithFlags(&d.res_stream, hipStreamNonBlocking));
-            for (hipEvent_t &e : d.slab_done) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIPCHECK(hipEventCreateWithFlags(&d.res_done, hipEventDisableTiming));
-        }
-        for (uint32_t k = 0; k < slabs; k++) {
-            const uint32_t ty0 = (uint32_t)((uint64_t)tyn * k / slabs), ty1 = (uint32_t)((uint64_t)tyn * (k + 1) / slabs);
-            launch_tile_raster(d.recs[p], W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p], list,
-                               d.keys, d.tile_list_cap[p], st, ty0, ty1, bcounts, bcap, d.tile_xoff);
-            HIPCHECK(hipEventRecord(d.slab_done[k], st));
-            HIPCHECK(hipStreamWaitEvent(d.res_stream, d.slab_done[k], 0));
-            launch_tile_resolve(d.keys, d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor,
-                                sw, sh, d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.res_stream, frame_rows,
-                                ty0 * th, std::min(rows_local, ty1 * th), g.tile_line_grid, d.deferred, d.tile_ctr[p]);
-        }
-        launch_tile_resolve_deferred(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
-                                     d.tex, g.ntex, out, d.deferred, d.tile_ctr[p], d.res_stream, bins,
-                                     d.tile_sum_dev + kSumWords * p);
-        HIPCHECK(hipEventRecord(d.res_done, d.res_stream));
-        HIPCHECK(hipStreamWaitEvent(st, d.res_done, 0));
-    }
+    launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
+                               d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
+                               list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff,
+                               d.tile_sum_dev + kSumWords * p);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());
@@ -982,6 +918,8 @@ void grow_tile_list(Dev &d, uint32_t p, uint64_t total) {
 // Spin until buffer set p's summary (k_tile_cursor / k_tile_bins_done) carries this frame's tag: a
 // stream synchronisation's wake-up costs ~10-20 us a frame; after 2 ms fall back to synchronising,
 // which also surfaces a device fault.
+bool bins_on(const Dev &d);
+
 void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
     volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     const auto t0 = std::chrono::steady_clock::now();
@@ -995,7 +933,9 @@ void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
             }
         }
     }
-    d.last_pairs = sum[2];
+    // (bins mode: word 2, the binned entries, is written by the frame's last kernel, after this
+    // point -- refresh_pairs reads it once the frame is done)
+    if (!bins_on(d)) d.last_pairs = sum[2];
     d.last_live = sum[1];
     d.last_kept = sum[3];
     d.tile_readbacks++;
@@ -1087,6 +1027,7 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
         // a (tile, bucket) outgrew its bin: bin the frame again into larger bins (or, past the budget,
         // into the lists), then its fragment stage
         d.tile_overflows++;
+        if (check_launches()) check_context(d.device, d.frame_no, "tile path, overflowed bins binned again");
         hipStream_t geo = d.geo[0];
         rebin(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
         tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
@@ -1164,13 +1105,6 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         d.scan_temp = dalloc<uint8_t>(d.scan_temp_bytes);
         d.tiles_cap = nt;
     }
-    const size_t npx = (size_t)W * rows_local;
-    if (d.keys_cap < npx) {                    // per-pixel winners (fragment stage, caller's stream)
-        HIPCHECK(hipDeviceSynchronize());
-        if (d.keys) HIPCHECK(hipFree(d.keys));
-        d.keys = dalloc<unsigned long long>(npx);
-        d.keys_cap = npx;
-    }
     // vertex stage (k_tile_vertex): measured on the 20 M-triangle stress scene at 4K, part 0 of 8
     // 1 996 -> 2 108 fps (setup 307 -> 235 us + 57 us for the stage), whole frame 826 -> 808 fps: on
     // for frame parts, where the per-triangle setup is replicated on every device; S3R_VERTEX_STAGE
@@ -1218,6 +1152,8 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     const bool readback_env = getenv("S3R_TILE_READBACK") && atoi(getenv("S3R_TILE_READBACK")) != 0;
     volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
     d.last_path = 2;
+    d.last_set = (int)p;
+    d.last_set_bins = bins;
     d.tile_H = H;
     if (bins) {
         // bins mode: asynchronous frames check the bins before their fragment stage (a spin on the
@@ -1255,7 +1191,6 @@ struct HostFill {
     uint32_t *probe_dev;
     unsigned long long *chunks_dev;
     uint32_t gpu_eighths;     // sky bins with bin % 8 below this stay with the GPU (adaptive split)
-    uint8_t *stage_dev;       // packed delivery: the device's address of the staging frame (or null)
 };
 
 // One frame part on device d (its current device must be set): rows_local rows of an interleaved
@@ -1271,6 +1206,9 @@ struct HostFill {
 void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                  uint32_t *out, hipStream_t st, const HostFill *hf = nullptr, bool sync = false) {
     TimingSlot *ts = timing_slot(d);
+    if (check_launches())
+        check_context(d.device, d.frame_no + 1u, use_tile_path() ? (sync ? "tile path, synchronous frame" : "tile path")
+                                                                  : (sync ? "row path, synchronous frame" : "row path"));
     if (use_tile_path()) {
         render_tiles(d, W, H, band, nparts, part, rows_local, out, st, ts, sync, hf != nullptr);
         return;
@@ -1371,8 +1309,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     launch_fragment(d.tris[p], 2 * g.ntri, d.rowtab[p], d.tex, g.ntex, out, W, H, band, nparts, part, rows_local,
                     d.bincnt[p], d.pairs[p], st, g.serial ? d.frag_done[p] : nullptr, d.done_dev, d.last_tag,
                     lpt ? d.order[p] : nullptr, hf != nullptr, hf && hf->flags_dev ? 1u + hf->gpu_eighths : 0u,
-                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u, row_starts,
-                    hf && hf->flags_dev ? hf->stage_dev : nullptr);
+                    hf ? hf->chunks_dev : nullptr, hf ? hf->tag : 0u, row_starts);
     d.issued_tag[p] = tag;
     d.last_tag = tag;
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
@@ -1749,15 +1686,6 @@ std::vector<cpu_set_t> fill_placement(int threads, int node) {
     return out;
 }
 
-// Packed delivery (host fill): whole covered chunks cross the link at 3 bytes a pixel into a
-// staging frame and the fill threads widen them into the caller's buffer (kernels.hip k_fragment,
-// host_fill.cpp widen_pixels) -- the link carries a quarter fewer bytes, the host writes the covered
-// pixels too.  Opt-in while its host side is tuned: S3R_PACK=1.
-bool pack_enabled() {
-    if (g.pack < 0) g.pack = getenv("S3R_PACK") && atoi(getenv("S3R_PACK")) == 1 ? 1 : 0;
-    return g.pack == 1;
-}
-
 // Fill threads for a frame of nparts device parts (S3R_FILL_THREADS / s3r_set_delivery override):
 // by default 4 (one device) or 8, but no more than the CPUs left beside the calling thread and the
 // nparts - 1 device workers.
@@ -1775,8 +1703,6 @@ int fill_threads(uint32_t nparts = 1) {
 }
 
 struct FillPart {
-    size_t stage_off;                // packed delivery: this part's bins in the staging frame (bytes)
-    uint32_t bin_bytes;              // ... one bin's staged pixels: rows x segment x 3 bytes, contiguous
     uint32_t *flags;                 // host view of the device's sky flags
     unsigned long long *chunks;      // host view of its covered bins' chunk masks
     uint32_t tag, seg_px, segs, rpb, chunk_px, rows_local, band, nparts, part;
@@ -1791,20 +1717,18 @@ struct FillJob {
     HostFill hf[kMaxDevices];
     std::atomic<bool> stale{false};  // pixel 0 checked before its bin was filled: the mapping is stale
     std::atomic<uint64_t> sky_px{0}; // background pixels the fill threads wrote
-    std::atomic<uint64_t> packed_px{0};  // staged pixels they widened (packed delivery)
-    const uint8_t *stage = nullptr;  // packed delivery: the staging frame (host address), else null
     std::chrono::steady_clock::time_point t0;
     std::atomic<int64_t> dev_end_ns{0}, fill_end_ns{0};   // latest finish of a device part / a fill thread
     // the adaptive split's measures: the first flag any thread saw, the last sky bin a thread filled,
     // and the sky bins of the frame (the host's and the GPUs')
     std::atomic<int64_t> flags_ns{INT64_MAX}, sky_end_ns{0};
     std::atomic<uint64_t> sky_bins{0};
-    std::atomic<uint64_t> part_px[kMaxDevices] = {}, part_packed[kMaxDevices] = {};   // per part, as sky_px / packed_px
+    std::atomic<uint64_t> part_px[kMaxDevices] = {};   // per part, as sky_px
     int64_t issued_ns = 0;                                 // part 0's launches issued
     std::chrono::steady_clock::time_point dev_done_ns[kMaxDevices];   // each device part's end
     int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
     uint64_t thread_px[65] = {};
-    int64_t thread_widen_ns[65] = {};  // time in covered bins (widening, their background chunks)
+    int64_t thread_covered_ns[65] = {};  // time in covered bins (their background chunks)
     int thread_cpu[65] = {};
 };
 
@@ -1816,21 +1740,11 @@ void note_end(const FillJob &job, std::atomic<int64_t> &end) {
 
 // Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
 // row_in_bin * chunks_per_row + chunk) of a covered bin; returns the pixels written.
-// Fills bin b's background -- the whole bin (sky), or the row chunks in mask (bit
-// row_in_bin * chunks_per_row + chunk) of a covered bin -- and, with the packed delivery, widens
-// the covered bin's staged chunks (every other chunk wholly inside the frame) into the frame;
-// returns the background pixels written, *packed += the pixels widened.
-uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, uint32_t mask, uint64_t *packed) {
+uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, uint32_t mask) {
     const uint32_t blk = (uint32_t)(b / fp.segs), seg = (uint32_t)(b % fp.segs);
     const uint32_t xs = seg * fp.seg_px, xe = xs + fp.seg_px < job.W ? xs + fp.seg_px : job.W;
     const uint32_t cpr = fp.seg_px / fp.chunk_px;
     uint64_t px = 0;
-    if (!sky && job.stage) {
-        // the bin's staged rows are cold (just written by the device): request all their lines at
-        // once, so the widening below waits for memory once per bin, not once per chunk
-        const uint8_t *a = job.stage + fp.stage_off + b * fp.bin_bytes, *e = a + fp.bin_bytes;
-        for (; a < e; a += 64) __builtin_prefetch(a, 0, 0);
-    }
     for (uint32_t k = 0; k < fp.rpb; k++) {
         const uint32_t lr = blk * fp.rpb + k;
         if (lr >= fp.rows_local) break;
@@ -1844,14 +1758,9 @@ uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, 
         }
         for (uint32_t q = 0; q < cpr; q++) {
             const uint32_t c0 = xs + q * fp.chunk_px, c1 = c0 + fp.chunk_px < xe ? c0 + fp.chunk_px : xe;
-            if (c0 >= c1) continue;
-            if ((mask >> (k * cpr + q)) & 1u) {
+            if (c0 < c1 && ((mask >> (k * cpr + q)) & 1u)) {
                 s3r_host::fill_words(row + c0, c1 - c0, kBackground);
                 px += c1 - c0;
-            } else if (job.stage && c1 - c0 == fp.chunk_px) {
-                s3r_host::widen_pixels(job.stage + fp.stage_off + b * fp.bin_bytes + 3 * ((size_t)k * fp.seg_px + (c0 - xs)),
-                                       row + c0, fp.chunk_px);
-                *packed += fp.chunk_px;
             }
         }
     }
@@ -1878,11 +1787,10 @@ void fill_worker(void *arg, int idx) {
         return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     };
     uint32_t idle = 0;
-    uint64_t px = 0, sky_bins = 0, packed = 0;
-    thread_local std::vector<uint64_t> ppx, ppk;            // per part: background / widened pixels
+    uint64_t px = 0, sky_bins = 0;
+    thread_local std::vector<uint64_t> ppx;                 // per part: background pixels
     ppx.assign((size_t)job.nparts, 0);
-    ppk.assign((size_t)job.nparts, 0);
-    int64_t widen_ns = 0;
+    int64_t covered_ns = 0;
     int64_t first_flag = -1, sky_end = 0;
     while (n) {
         size_t keep = 0;
@@ -1905,45 +1813,39 @@ void fill_worker(void *arg, int idx) {
                 const unsigned long long c = __atomic_load_n(fp.chunks + b, __ATOMIC_ACQUIRE);
                 if ((uint32_t)(c >> 32) != fp.tag) { pend[keep++] = e; continue; }
                 mask = (uint32_t)c;
-                if (!mask && !job.stage) continue;
+                if (!mask) continue;
             }
             // pixel 0 (part 0, bin 0, its first row and chunk): the flag publisher wrote kMapProbe
             // there through its mapping before publishing the bin's flag; the host writes pixel 0 when
-            // the chunk is background or staged (packed delivery)
-            if (part == 0 && b == 0 && (sky || (mask & 1u) || (job.stage && fp.rows_local && job.W >= fp.chunk_px)) &&
-                __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
+            // the chunk is background
+            if (part == 0 && b == 0 && (sky || (mask & 1u)) && __atomic_load_n(job.frame, __ATOMIC_ACQUIRE) != kMapProbe)
                 job.stale.store(true, std::memory_order_relaxed);
-            const uint64_t px0 = px, pk0 = packed;
-            if (!sky && job.stage) {
+            const uint64_t px0 = px;
+            if (!sky) {
                 const auto w0 = std::chrono::steady_clock::now();
-                px += fill_bin(job, fp, b, sky, mask, &packed);
-                widen_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+                px += fill_bin(job, fp, b, sky, mask);
+                covered_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             } else {
-                px += fill_bin(job, fp, b, sky, mask, &packed);
+                px += fill_bin(job, fp, b, sky, mask);
             }
             ppx[part] += px - px0;
-            ppk[part] += packed - pk0;
             if (sky) sky_end = since_start();
         }
         if (keep == n) {
             __builtin_ia32_pause();
             if ((++idle & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
-                // a device that never published these bins (a fault surfaces in the device part's
-                // stream synchronisation): give up on the frame -- it is redone by copy
-                fprintf(stderr, "s3r: host fill: %zu bins never flagged in 20 s; frame redone by copy\n", keep);
-                job.stale.store(true, std::memory_order_relaxed);
-                break;
+                // every device part has been synchronised by the time a frame takes this long, so a
+                // bin never flagged is a protocol bug, not a slow device: fail loudly
+                fprintf(stderr, "s3r: host fill: %zu bins never flagged in 20 s (flag protocol broken)\n", keep);
+                abort();
             }
         }
         n = keep;
     }
     s3r_host::store_fence();
     job.sky_px.fetch_add(px, std::memory_order_relaxed);
-    job.packed_px.fetch_add(packed, std::memory_order_relaxed);
-    for (int p = 0; p < job.nparts; p++) {
+    for (int p = 0; p < job.nparts; p++)
         if (ppx[p]) job.part_px[p].fetch_add(ppx[p], std::memory_order_relaxed);
-        if (ppk[p]) job.part_packed[p].fetch_add(ppk[p], std::memory_order_relaxed);
-    }
     job.sky_bins.fetch_add(sky_bins, std::memory_order_relaxed);
     if (first_flag >= 0) {
         int64_t cur = job.flags_ns.load(std::memory_order_relaxed);
@@ -1954,7 +1856,7 @@ void fill_worker(void *arg, int idx) {
         while (sky_end > cur && !job.sky_end_ns.compare_exchange_weak(cur, sky_end, std::memory_order_relaxed)) {}
     }
     job.thread_px[idx] = px;
-    job.thread_widen_ns[idx] = widen_ns;
+    job.thread_covered_ns[idx] = covered_ns;
     job.thread_cpu[idx] = sched_getcpu();
     job.thread_end_ns[idx] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
     note_end(job, job.fill_end_ns);
@@ -2073,45 +1975,12 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
         fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.chunk_px = l.chunk_px;
         fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
-        fp.bin_bytes = fp.rpb * fp.seg_px * 3u;
-        fp.stage_off = i == 0 ? 0 : job.parts[i - 1].stage_off + job.parts[i - 1].bins * job.parts[i - 1].bin_bytes;
-    }
-    // packed delivery (host fill only): the staging frame, 3 bytes a pixel, mapped on every device
-    if (fill && pack_enabled()) {
-        // ordinary (CPU-cacheable) pages, registered plainly for the devices: the fill threads read
-        // it at memory speed (hipHostMalloc's pages, or an uncached registration, read ~10x slower);
-        // its rows are 64-B aligned, so the GPUs' whole-line stores need no uncached mapping
-        // bin-major: each bin's rows x segment pixels contiguous (the fill threads stream through their
-        // blocks of bins instead of gathering a bin's 1-KB row pieces, 3 W bytes apart)
-        const FillPart &lp = job.parts[nparts - 1];
-        const size_t bytes = (lp.stage_off + lp.bins * lp.bin_bytes + 64 + 4095) & ~(size_t)4095;
-        if (g.stage_cap < bytes) {
-            drain_devices();
-            HIPCHECK(hipSetDevice(g.devs[0]->device));
-            free_stage();
-            void *p = aligned_alloc(4096, bytes);
-            if (!p) { fprintf(stderr, "s3r: staging frame allocation failed\n"); exit(1); }
-            memset(p, 0, bytes);
-            HIPCHECK(hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
-            g.stage = static_cast<uint8_t *>(p);
-            g.stage_cap = bytes;
-            g.stage_epoch++;
-        }
-        job.stage = g.stage;
-        for (uint32_t i = 0; i < nparts; i++) {
-            Dev &d = *g.devs[i];
-            if (d.stage_epoch != g.stage_epoch) {
-                HIPCHECK(hipSetDevice(d.device));
-                HIPCHECK(hipHostGetDevicePointer((void **)&d.stage_dev, g.stage, 0));
-                d.stage_epoch = g.stage_epoch;
-            }
-        }
     }
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
         FillPart &fp = job.parts[i];
         if (!fill) {
-            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0, nullptr};
+            job.hf[i] = HostFill{nullptr, 0, nullptr, nullptr, 0};
             continue;
         }
         if (d.fill_cap < fp.bins) {
@@ -2136,8 +2005,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
         fp.flags = d.fill_flags;
         fp.chunks = d.fill_chunks;
         fp.tag = d.fill_tag;
-        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu,
-                             job.stage ? d.stage_dev + fp.stage_off : nullptr};
+        job.hf[i] = HostFill{d.fill_flags_dev, d.fill_tag, nullptr, d.fill_chunks_dev, (uint32_t)g.fill_gpu};
     }
     HIPCHECK(hipSetDevice(g.devs[0]->device));
     buffer[0] = kStaleProbe;      // overwritten through the mapping (a pixel, or k_sky_flags' probe)
@@ -2158,7 +2026,7 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
             g.prof_thread[t].cpu = job.thread_cpu[t];
             g.prof_thread[t].end_ns += (uint64_t)job.thread_end_ns[t];
             g.prof_thread[t].px += job.thread_px[t];
-            g.prof_thread[t].covered_ns += (uint64_t)job.thread_widen_ns[t];
+            g.prof_thread[t].covered_ns += (uint64_t)job.thread_covered_ns[t];
         }
     }
     if (fill && !getenv("S3R_FILL_GPU") && job.flags_ns.load() != INT64_MAX) fill_adapt(job, nparts);
@@ -2167,20 +2035,29 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
     bool host0 = false;
     if (fill && job.parts[0].bins) {
         const uint32_t f0 = job.parts[0].flags[0];
-        host0 = (f0 & kSkyBit) ||
-                (!(f0 & kGpuBit) && ((job.parts[0].chunks[0] & 1ull) || (job.stage && W >= job.parts[0].chunk_px)));
+        host0 = (f0 & kSkyBit) || (!(f0 & kGpuBit) && (job.parts[0].chunks[0] & 1ull));
     }
     const bool stale = job.stale.load() || (!host0 && (buffer[0] == kStaleProbe || buffer[0] == kMapProbe));
+    if (stale) return kStaleMap;             // (redone by copy, which profiles the frame itself)
     (fill ? g.fill_frames : g.direct_frames)++;
-    g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load() - job.packed_px.load()) + 3 * job.packed_px.load();
+    g.link_bytes = 4 * ((uint64_t)W * H - job.sky_px.load());
     for (uint32_t i = 0; i < nparts; i++) {
         Lib::DevProf &dp = g.dev_prof[i];
-        const uint64_t px = (uint64_t)job.parts[i].rows_local * W, sky = job.part_px[i].load(), pk = job.part_packed[i].load();
+        const uint64_t px = (uint64_t)job.parts[i].rows_local * W, sky = job.part_px[i].load();
         dp.frames++;
         dp.end_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(job.dev_done_ns[i] - g.call_t0).count();
-        dp.link_bytes = 4 * (px - sky - pk) + 3 * pk;
+        dp.link_bytes = 4 * (px - sky);
     }
-    return stale ? kStaleMap : kMapped;
+    return kMapped;
+}
+
+// Bins mode: the last tile-path frame's binned-entry total (summary word 2) is written by its last
+// kernel; the statistics read it once the device is drained.
+void refresh_pairs(Dev &d) {
+    if (d.last_path != 2 || !d.last_set_bins || d.last_set < 0 || !d.tile_sum_host) return;
+    HIPCHECK(hipSetDevice(d.device));
+    HIPCHECK(hipDeviceSynchronize());
+    d.last_pairs = __atomic_load_n(d.tile_sum_host + kSumWords * (uint32_t)d.last_set + 2, __ATOMIC_ACQUIRE);
 }
 
 }  // namespace
@@ -2478,6 +2355,7 @@ __attribute__((visibility("default"))) void s3r_timing_collect(double out[3]) {
 }
 
 __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
+    if (!g.devs.empty()) refresh_pairs(*g.devs[0]);
     const Dev *d = g.devs.empty() ? nullptr : g.devs[0];
     out[0] = g.nv; out[1] = g.nindices; out[2] = g.na; out[3] = g.ntex; out[4] = 2ull * g.ntri;
     out[5] = d ? d->last_pairs : 0;          // tile path: (slot, tile) pairs binned last frame
@@ -2486,6 +2364,7 @@ __attribute__((visibility("default"))) void s3r_scene_counts(uint64_t out[8]) {
 }
 
 __attribute__((visibility("default"))) void s3r_tile_stats(uint64_t out[4]) {
+    if (!g.devs.empty()) refresh_pairs(*g.devs[0]);
     const Dev *d = g.devs.empty() ? nullptr : g.devs[0];
     out[0] = d ? d->tile_readbacks : 0;      // frames whose list size was read back before the fill
     out[1] = d ? d->tile_overflows : 0;      // synchronous frames rendered again into a larger list

@@ -6,6 +6,14 @@
 
 namespace s3r {
 
+// S3R_CHECK=1 (diagnostics): every launcher below synchronises its stream after each kernel it
+// launches and checks for a device fault; a fault is reported with the kernel's name and the
+// calling thread's frame context (check_context: device, frame number, stage) and the process
+// aborts -- a fault then names the launch that caused it instead of surfacing in a later HIP call.
+bool check_launches();
+void check_context(int device, uint32_t frame, const char *stage);
+void after_launch(const char *kernel, hipStream_t st);
+
 // `done` (may be null): recorded on `st` when the launched kernel completes.
 // order (may be null: launch order): 2 x fragment_bins() words, [perm | cost] -- launch_geometry's
 // extra workgroup (order non-null there) writes perm, the launch's workgroup -> bin map, from the
@@ -18,18 +26,13 @@ namespace s3r {
 // write nothing -- the host fills them (launch_sky_flags) -- and neither do the row chunks of covered
 // bins that end without a winner:
 // each bin's workgroup stores chunk_flags[bin] = (fill_tag << 32) | mask at its end, bit
-// (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.  stage (with
-// frame_rows and host_fill; device address of a host buffer of bins x rows_per_bin x segment x 3
-// bytes): every other chunk that lies wholly inside the frame is stored there packed at 3 bytes a
-// pixel (bin-major: bin b at stage + b x rows_per_bin x segment x 3, its row r at + r x segment x
-// 3, the chunk at + 3 x (x - segment start); little-endian b, g, r) instead of into out, for the
-// host to widen (complete before the mask).
+// (row_in_bin * chunks_per_row + chunk) for every such chunk, for the host to fill.
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,
                      uint32_t *out, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
                      uint32_t rows_local, uint32_t *bincnt, const uint4 *pairs,
                      hipStream_t st, hipEvent_t done, uint32_t *done_flag, uint32_t prev_tag, uint32_t *order,
                      bool frame_rows = false, uint32_t host_fill = 0, unsigned long long *chunk_flags = nullptr,
-                     uint32_t fill_tag = 0, bool row_starts = false, uint8_t *stage = nullptr);
+                     uint32_t fill_tag = 0, bool row_starts = false);
 
 // Fragment workgroups (bins = blocks of 4 local rows x segments) and their triangle lists: per bin a
 // pair count -- k_geometry counts up from 0, the bin's fragment workgroup reads it and resets it to 0
@@ -148,15 +151,6 @@ void launch_tile_cursor(const uint32_t *counts, const uint32_t *offs, uint32_t W
 void launch_tile_fill(const uint4 *live, uint32_t *ctr, const TileClusters *cl, uint32_t ntri, uint32_t W,
                       uint32_t band, uint32_t nparts, uint32_t part, uint32_t *cursor, uint32_t *list, uint64_t cap,
                       hipStream_t st, uint32_t xoff = 0);
-// keys: rows_local x W u64 per-pixel winners (bits(1/z) << 32 | ~slot), 0 = no fragment.
-// ctr: the setup's counters (its list length ctr[1]; the launch of tile row 0 resets the live counters
-// when the list did not overflow).
-void launch_tile_raster(const void *recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                        uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
-                        unsigned long long *keys, uint64_t cap, hipStream_t st,
-                        uint32_t ty0 = 0, uint32_t ty1 = 0xFFFFFFFFu,    // tile rows [ty0, ty1) only
-                        uint32_t *counts = nullptr, uint32_t bin_cap = 0,    // bins mode: list = tbin
-                        uint32_t xoff = 0);
 // Raster and resolve in one launch (each tile shades its winners from LDS and stores them into out:
 // its local rows, or with frame_rows the frame rows of a W x H frame), then the pixels whose winner
 // needs a full setup (ctr[3] of them, in `deferred`: W x rows_local entries) in a second, short one.
@@ -168,14 +162,6 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows,
                                 uint32_t *counts = nullptr, uint32_t bin_cap = 0, uint32_t xoff = 0,
                                 uint32_t *sum_host = nullptr);      // bins: the entries' total (launch_tile_resolve_deferred)
-void launch_tile_resolve(const unsigned long long *keys, const void *recs, const float4 *vtx, const float4 *nrm,
-                         const float4 *pay, const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx,
-                         uint32_t ntri, const Mat34 &m, float factor, float sw, float sh, const uint32_t *tex,
-                         uint32_t ntex, uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
-                         uint32_t rows_local, hipStream_t st, bool frame_rows,
-                         uint32_t r0, uint32_t r1,           // local rows [r0, r1) only (r0 % 4 == 0)
-                         bool line_grid,                     // frame_rows: wave stores on the caller's 64-B line grid
-                         uint4 *deferred, uint32_t *ctr);    // pixels whose winner needs its full setup (ctr[3])
 // Those pixels, shaded with the winner's full setup (after every resolve launch of the frame).
 void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
                                   const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,

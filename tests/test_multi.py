@@ -296,3 +296,32 @@ finally:
     res = subprocess.run([sys.executable, '-c', code], cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert res.returncode == 0, res.stderr[-2000:]
     assert np.array_equal(np.load(out), want)
+
+
+@pytest.mark.gpu
+def test_nccl_gather_in_process(gpu_renderer, scene_dir):
+    """The same RCCL gather in THIS process, with the session's library (round 4's form of the test,
+    when two later GPU tests aborted with hipErrorIllegalAddress).  Opt-in (S3R_TEST_RCCL_INPROCESS=1):
+    the experiment that decides whether a torn-down in-process communicator is the cause runs it
+    first, then the tile and multi-device suites, under S3R_CHECK=1 (every library launch checked)."""
+    if os.environ.get('S3R_TEST_RCCL_INPROCESS') != '1':
+        pytest.skip('opt-in: S3R_TEST_RCCL_INPROCESS=1')
+    from oracle.oracle import render_pose
+    from swift3drenderer_amd import poses
+    w, h = 640, 480
+    script = poses.script('P_over')
+    want = render_pose(scene_dir['full'], script, w, h)
+    r = gpu_renderer
+    r.configure(scene_dir['full'])
+    for t in script:
+        r.update_and_render(w, h, t)
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{free_port()}', rank=0, world_size=1)
+    try:
+        bg = BandGather(w, h, 16, 1, 0, torch.device('cuda'))
+        r.render_bands(poses.hold('P_over'), w, h, 16, 1, 0, bg.send.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+        got = bg.gather()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), want)

@@ -244,25 +244,3 @@ def test_host_fill_thread_placement(multi, scene_dir, monkeypatch, pin):
             assert len({dom[t['cpu']] for t in prof['threads']}) == 4, (prof, dom)
     finally:
         multi.set_delivery('env')
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize('pack', ['1', '0'])
-@pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
-def test_host_fill_packed_matches_oracle(multi, scene_dir, monkeypatch, pack, devices):
-    """Host fill with the packed delivery (whole covered chunks staged at 3 bytes a pixel and widened
-    by the fill threads; chunks cut by the right edge stored directly) and without it: the oracle's
-    frames at widths that are and are not multiples of the 64-px chunk, 1 and 3 parts."""
-    monkeypatch.setenv('S3R_PACK', pack)
-    monkeypatch.setenv('S3R_FILL_GPU', '0')          # every sky bin to the host: link bytes = covered chunks
-    multi.set_delivery('fill')
-    try:
-        for (w, h, pose) in [(1000, 333, 'P_over'), (640, 480, 'P_clip'), (17, 5, 'P_id'), (3840, 2160, 'P_over')]:
-            frames_vs_oracle(multi, scene_dir['full'], pose_frames(pose, w, h), devices)
-        st = multi.host_stats()
-        assert st['fill_frames'] > 0, st
-        if pack == '1':
-            # covered chunks crossed the link packed: fewer bytes than their 4-byte pixels
-            assert st['link_bytes'] < 13_690_112, st
-    finally:
-        multi.set_delivery('env')

@@ -360,19 +360,14 @@ def test_tile_deliveries_match_oracle(gpu_renderer, icosa_dir, monkeypatch, mode
 
 
 @pytest.mark.parametrize('line', ['1', '0'])
-@pytest.mark.parametrize('slabs', ['1', '3', '16'])
 @pytest.mark.parametrize('devices', [[0], [0, 0]])
-def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, devices, line):
-    """Direct tile-path frames rendered in row slabs (S3R_TILE_SLABS: slab k's resolve on a second
-    stream while slab k + 1 rasterizes) equal the oracle's, for slab counts that divide the tile rows
-    unevenly or exceed them, frame heights that end inside a tile, and two parts; with the resolve's
-    waves on the caller's 64-B line grid (S3R_TILE_LINE=1, the default: rows starting mid-line, an
-    odd width) and without.  The split raster / resolve launches (S3R_TILE_FUSED=0; whole frames are
-    fused by default)."""
+def test_tile_direct_frames_match_oracle(gpu_renderer, icosa_dir, monkeypatch, devices, line):
+    """Direct tile-path frames (the fused raster writes every pixel at its frame row of the caller's
+    mapped buffer) equal the oracle's through resizes, frame heights that end inside a tile and odd
+    widths, on one and two parts; with the tile grid on the caller's 64-B line grid (S3R_TILE_LINE=1,
+    the default) and without."""
     from oracle.oracle import OracleRenderer
-    monkeypatch.setenv('S3R_TILE_SLABS', slabs)
     monkeypatch.setenv('S3R_TILE_LINE', line)
-    monkeypatch.setenv('S3R_TILE_FUSED', '0')          # (the slabs are the split raster / resolve's)
     r = gpu_renderer
     r.configure_devices(devices)
     path = icosa_dir[2000]
@@ -387,7 +382,7 @@ def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, de
             out = np.full((h, w), 0x5A5A5A5A, dtype=np.uint32)
             got = r.update_and_render(w, h, inp, out)
             want = o.update_and_render(w, h, inp)
-            assert np.array_equal(got, want), f'frame {k} {w}x{h} slabs {slabs}: ' + diff(got, want)
+            assert np.array_equal(got, want), f'frame {k} {w}x{h} line {line}: ' + diff(got, want)
         assert r.raster_path() == 'tiles'
         assert r.host_stats()['direct_frames'] == len(seq)
     finally:
@@ -398,12 +393,11 @@ def test_tile_slabs_match_oracle(gpu_renderer, icosa_dir, monkeypatch, slabs, de
 @pytest.mark.parametrize('case', [('full', 'P_clip', 640, 480, 1), ('full', 'P_over', 1000, 333, 1),
                                   ('stress', 'P_id', 1920, 1080, 1), ('stress', 'P_strafe', 1280, 720, 3)])
 def test_fused_raster_resolve_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeypatch, case):
-    """Raster and resolve in one launch (S3R_TILE_FUSED=1): each tile shades its winners from LDS;
-    pixels whose winner was clipped at the near plane (P_clip) go through the deferred pass.  Whole
-    frames, a 3-part split, and direct delivery into the caller's buffer."""
+    """Raster and resolve in one launch: each tile shades its winners from LDS; pixels whose winner
+    was clipped at the near plane (P_clip) go through the deferred pass.  Whole frames, a 3-part
+    split, and direct delivery into the caller's buffer."""
     import torch
     from swift3drenderer_amd.multi import assemble
-    monkeypatch.setenv('S3R_TILE_FUSED', '1')
     name, pose, w, h, nparts = case
     path = icosa_dir[2000] if name == 'stress' else scene_dir[name]
     r = gpu_renderer
