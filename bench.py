@@ -13,7 +13,11 @@ allocates it: ONE malloc of 2 * bufferSize whose halves are used alternately (ma
 N GPUs: the reference's caller is one process on one thread, so the N GPUs sit behind that one call
 (s3r_configure_devices): rank 0 calls updateAndRender with devices 0..N-1, each rendering its
 interleaved 16-row bands and copying them into their rows of the caller's buffer over its own PCIe
-link.  Ranks 1..N-1 only take part in the barriers (gloo).  Scaling is strong (a fixed frame).
+link -- that is ``value``.  Then every rank renders its own part on its own GPU (one process per GPU,
+``ranks``): the part left in HBM (``device_fps_N`` = frames / the slowest rank's time) and the
+parts gathered to rank 0 over xGMI by one RCCL gather plus the de-interleave kernel
+(``gathered_fps``), each with its per-GPU efficiency against rank 0's whole frame on one GPU.
+Scaling is strong (a fixed frame).
 
 Beside ``value``: ``device_fps`` (one GPU, frames pipelined and left in HBM: s3r_render_bands),
 the ``roofline`` of the fragment kernel (HIP events on its stream during updateAndRender frames),
@@ -47,7 +51,7 @@ MIN_TIMED = 200          # >= 200 frames after 20 warm-up fram
 MIN_WARMUP = 20
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=MIN_TIMED)
@@ -67,7 +71,15 @@ def parse():
     p.add_argument('--no-device', action='store_true', help='skip the device-resident (HBM) rate')
     p.add_argument('--data', default=None,
                    help='data.bin path to reuse across runs (the deterministic scene is written there when missing)')
-    return p.parse_args()
+    p.add_argument('--ranks-leg', action='store_true',
+                   help='run the one-process-per-GPU leg (on by default when WORLD_SIZE > 1; with one rank: '
+                        'the single-rank RCCL gather)')
+    p.add_argument('--rank-devices', default=None,
+                   help='comma-separated GPU of each rank in the ranks leg (default: LOCAL_RANK); repeated '
+                        'ids rehearse ranks on one GPU and then need --gather-backend gloo')
+    p.add_argument('--gather-backend', default='nccl', choices=('nccl', 'gloo'),
+                   help='the ranks leg\'s gather: nccl (RCCL over xGMI) or gloo (a rehearsal through host copies)')
+    return p.parse_args(argv)
 
 
 def cpu_model() -> str:
@@ -171,8 +183,8 @@ class DoubleBuffer:
         self.libc.free(self.raw)
 
 
-def main():
-    a = parse()
+def main(argv=None):
+    a = parse(argv)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -182,23 +194,184 @@ def main():
     if world == 1 and a.gpus > 1:
         raise SystemExit('--gpus N>1 needs torch.distributed.run with N processes')
     N = max(world, 1)
-    if world > 1:
+    ranks_on = world > 1 or a.ranks_leg
+    if world > 1 or ranks_on:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        # control only (barriers, the max over ranks): the frame's data path is inside rank 0's call
+        os.environ.setdefault('MASTER_PORT', '29511')
+        os.environ.setdefault('RANK', '0')
+        os.environ.setdefault('WORLD_SIZE', '1')
+        # control (barriers, the max over ranks); the ranks leg's gather has its own group
         dist.init_process_group('gloo')
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
 
     result = None
     if rank == 0:
         result = run_rank0(a, N, np, torch)
+    barrier()
+    if ranks_on:
+        rl = run_ranks_leg(a, rank, N, np, torch, dist,
+                           result['device_fps'] if rank == 0 and result else None)
+        if rank == 0:
+            result['ranks'] = rl
+    if rank == 0:
         print(json.dumps(result), flush=True)
     barrier()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return result
+
+
+def rank_device(a, rank, torch):
+    """The GPU of this rank in the ranks leg: --rank-devices, else LOCAL_RANK."""
+    if a.rank_devices:
+        ids = [int(x) for x in a.rank_devices.split(',')]
+        return ids[rank % len(ids)]
+    return int(os.environ.get('LOCAL_RANK', str(rank)))
+
+
+def ranks_leg(render_part, render_whole, sync, gather, barrier, allgather_f, W, H, B, N, rank, steps, warmup,
+              clock=time.perf_counter):
+    """One process per GPU: this rank's part of every frame.
+
+    render_part(): issue one frame of this rank's interleaved bands into its send buffer (asynchronous);
+    gather(): the collective that brings every rank's part to rank 0 and de-interleaves it there
+    (returns rank 0's frame, else None); render_whole(): rank 0's reference, the whole frame on its one
+    GPU (None elsewhere); sync(): the device drained; barrier(); allgather_f(x): every rank's float.
+    Returns, on every rank, per-rank part times and the max over ranks of the device-resident pass and
+    of the gathered pass (each K frames, barrier + sync on both sides), and whether rank 0's gathered
+    frame equals its whole frame."""
+    for _ in range(warmup):
+        render_part()
+    sync()
+
+    def timed(body):
+        barrier()
+        sync()
+        t0 = clock()
+        for _ in range(steps):
+            body()
+        sync()
+        t = clock() - t0
+        barrier()
+        return allgather_f(t)
+
+    dev_times = timed(render_part)
+
+    def frame():
+        render_part()
+        gather()
+
+    for _ in range(max(2, warmup // 4)):
+        frame()
+    sync()
+    gat_times = timed(frame)
+    render_part()
+    got = gather()
+    sync()
+    same = None
+    if rank == 0 and render_whole is not None:
+        want = render_whole()
+        sync()
+        same = bool(got is not None and want is not None and got.shape == want.shape and bool((got == want).all()))
+    return {'device_s': dev_times, 'gathered_s': gat_times, 'gathered_equals_whole': same}
+
+
+def run_ranks_leg(a, rank, N, np, torch, dist, device_fps_1):
+    """The ranks leg on this rank: its own GPU, its own library state, the part it owns."""
+    from swift3drenderer_amd import poses, scene
+    from swift3drenderer_amd.abi import Input
+    from swift3drenderer_amd.multi import BandGather, band_rows
+    from swift3drenderer_amd.renderer import Renderer
+
+    dev_id = rank_device(a, rank, torch)
+    torch.cuda.set_device(dev_id)
+    dev = torch.device('cuda', dev_id)
+    tmp = tempfile.mkdtemp(prefix=f's3r_rank{rank}_')
+    data_path = os.path.join(tmp, f'{a.scene}.bin')
+    scene.write_named(a.scene, data_path)
+    W, H = a.width, a.height
+    r = Renderer(data_path, device=dev_id)
+    B = a.band or r.frame_band(H, N)
+    if N == 1:
+        B = H
+    script, hold_in = poses.script(a.pose), Input.of(poses.hold(a.pose))
+    st = torch.cuda.current_stream(dev)
+    nccl = a.gather_backend == 'nccl'
+    group = dist.new_group(backend='nccl') if nccl else None
+    bg = BandGather(W, H, B, N, rank, dev)
+    if not nccl:
+        cpu = BandGather(W, H, B, N, rank, torch.device('cpu'))
+    for t in script:
+        r.render_bands(t, W, H, B, N, rank, bg.send.data_ptr(), st.cuda_stream)
+
+    def render_part():
+        r.render_bands(hold_in, W, H, B, N, rank, bg.send.data_ptr(), st.cuda_stream)
+
+    def gather():
+        if nccl:
+            return bg.gather(group=group)
+        cpu.send.copy_(bg.send)                       # rehearsal: through host copies over gloo
+        out = cpu.gather()
+        return out.to(dev) if rank == 0 else None
+
+    whole = None
+    if rank == 0:
+        ref = torch.empty((H, W), dtype=torch.int32, device=dev)
+
+        def whole():
+            r2 = Renderer(data_path, device=dev_id)   # (the library is per process: a fresh state, whole frame)
+            for t in script:
+                r2.render_bands(t, W, H, H, 1, 0, ref.data_ptr(), st.cuda_stream)
+            r2.render_bands(hold_in, W, H, H, 1, 0, ref.data_ptr(), st.cuda_stream)
+            return ref
+
+    def allgather_f(x):
+        out = [None] * N
+        dist.all_gather_object(out, float(x))
+        return out
+
+    steps = max(a.steps, MIN_TIMED)
+    res = ranks_leg(render_part, whole, lambda: torch.cuda.synchronize(dev), gather, dist.barrier, allgather_f,
+                    W, H, B, N, rank, steps, max(a.warmup, MIN_WARMUP))
+    r.shutdown()
+    shutil.rmtree(tmp, ignore_errors=True)
+    if rank != 0:
+        return None
+    return ranks_summary(res, W, H, B, N, steps, device_fps_1, [band_rows(H, B, N, p) for p in range(N)],
+                         'rccl (torch.distributed nccl) gather + s3r_deinterleave_bands' if nccl else
+                         'gloo gather through host copies (rehearsal) + index_select')
+
+
+def ranks_summary(res, W, H, B, N, steps, device_fps_1, rows, gather_desc):
+    """The ranks leg's JSON: per-rank frame times, the slowest rank, device-resident and gathered
+    frames/s and their per-GPU efficiency fps(N) / (N fps(1)), fps(1) = rank 0's whole frame on one
+    GPU in this run (device_fps)."""
+    dev_ms = [t / steps * 1e3 for t in res['device_s']]
+    gat_ms = [t / steps * 1e3 for t in res['gathered_s']]
+    dfps = steps / max(res['device_s'])
+    gfps = steps / max(res['gathered_s'])
+    eff = (lambda f: round(f / (N * device_fps_1), 4)) if device_fps_1 else (lambda f: None)
+    return {
+        'processes': N, 'band_rows': B, 'rows_per_rank': rows,
+        'per_rank_device_ms': [round(x, 5) for x in dev_ms],
+        'max_rank_device_ms': round(max(dev_ms), 5),
+        'device_fps_N': round(dfps, 3),
+        'device_mpixels_per_s': round(dfps * W * H / 1e6, 2),
+        'device_efficiency_per_gpu': eff(dfps),
+        'per_rank_gathered_ms': [round(x, 5) for x in gat_ms],
+        'gathered_fps': round(gfps, 3),
+        'gathered_efficiency_per_gpu': eff(gfps),
+        'fps_1': round(device_fps_1, 3) if device_fps_1 else None,
+        'gather': gather_desc,
+        'gathered_equals_whole_frame': res['gathered_equals_whole'],
+        'note': 'every rank renders its interleaved bands of the frame on its own GPU (s3r_render_bands, '
+                'frames pipelined, left in HBM); device_fps_N = frames / the slowest rank\'s time; gathered_fps '
+                'adds one gather of the parts to rank 0 and the de-interleave per frame; efficiency = fps(N) / '
+                '(N x fps(1)), fps(1) = rank 0\'s whole frame on one GPU (device_fps)',
+    }
 
 
 def run_rank0(a, N, np, torch):

@@ -85,7 +85,7 @@ class OracleRenderer:
         a test extension for checking full-size frames on a few rows (render_oracle.c)."""
         flat = (ctypes.c_uint32 * max(1, 2 * len(windows)))(*[v for w in windows for v in w])
         if self._lib().oracle_set_row_windows(flat, len(windows)) != 0:
-            raise ValueError('at most 16 row windows')
+            raise ValueError('at most 32 row windows')
 
     def camera_matrix(self) -> np.ndarray:
         m = (ctypes.c_float * 12)()

@@ -331,7 +331,7 @@ static void clip(data_t *data, uint64_t *v_count, uint64_t *a_count, uint64_t *v
  * walked -- wy += dy once per row (render.cpp:378), exactly as the loop below does -- but not
  * rasterised, so a full-size frame (the 20 M-triangle stress scene) can be checked on a few rows in
  * seconds.  A row's pixels depend only on its walk state, so the windows' rows are the reference's. */
-#define ORACLE_MAX_WINDOWS 16
+#define ORACLE_MAX_WINDOWS 32
 static uint32_t win_count = 0, win_rows[2 * ORACLE_MAX_WINDOWS];
 static int row_in_windows(uint32_t y) {
     if (!win_count) return 1;
@@ -494,7 +494,7 @@ void oracle_updateAndRender(const PixelData *pixel_data, const Input *input) {
     render_frame(pixel_data, input);
 }
 
-/* Row windows [rows[2i], rows[2i+1]), i < n (n <= 16; n = 0: every row) -- see row_in_windows. */
+/* Row windows [rows[2i], rows[2i+1]), i < n (n <= 32; n = 0: every row) -- see row_in_windows. */
 int oracle_set_row_windows(const uint32_t *rows, uint32_t n) {
     if (n > ORACLE_MAX_WINDOWS) return -1;
     for (uint32_t i = 0; i < 2 * n; i++) win_rows[i] = rows[i];

@@ -1858,6 +1858,9 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
         if (sp.n) {
             bx = bt;
             by = ts.ymin | (ts.ymax << 16);
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 32)
+            if (slot == 0xFFFFFFFFu)                    // ablation: no raster record written
+#endif
             write_rec(recs + slot, ts, slot, zb);
         }
     }

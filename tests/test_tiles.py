@@ -198,7 +198,9 @@ def test_forced_clusters_packaged(tiles, scene_dir, monkeypatch, scene_name, pos
 def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
     """BASELINE config 5 at full size: 1 000 000 icosahedra (20 M triangles) at 3840x2160.  The GPU
     frame is whole; the oracle draws only a few row windows (every other row is walked, not drawn --
-    oracle_set_row_windows), and those rows must match bit for bit."""
+    oracle_set_row_windows), and those rows must match bit for bit.  Also config 5's actual 8-GPU
+    split: all 8 parts at the library's own tile-path band (s3r_frame_band: two 135-row bands per
+    part), each part checked on a window inside each of its two bands."""
     from oracle.oracle import OracleRenderer
     path = str(tmp_path / 'icosa-stress.bin')
     stress.write_named('icosa-stress', path)
@@ -215,9 +217,21 @@ def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
         r.render_bands(inp, W, H, 16, 8, 3, buf.data_ptr(), 0)
         torch.cuda.synchronize()
         part = buf.cpu().numpy().view(np.uint32)
+        # the 8-way split at the library's band (what updateAndRender over 8 devices uses)
+        band8 = r.frame_band(H, 8)
+        assert band8 == 135
+        parts8 = []
+        for p in range(8):
+            rows_p = r.lib.s3r_band_rows_local(H, band8, 8, p)
+            b = torch.empty((rows_p, W), dtype=torch.int32, device='cuda')
+            r.render_bands(inp, W, H, band8, 8, p, b.data_ptr(), 0)
+            torch.cuda.synchronize()
+            parts8.append(b.cpu().numpy().view(np.uint32))
     finally:
         r.configure(None)                           # drop the 4 GB scene; back to the packaged data.bin
-    wins = [(0, 16), (48, 64), (700, 716), (1072, 1097), (2144, 2160)]
+    # one 6-row window inside each 135-row band: bands b and b + 8 belong to part b
+    wins8 = [(135 * b + 70 + 4 * (b % 5), 135 * b + 76 + 4 * (b % 5)) for b in range(16)]
+    wins = sorted([(0, 16), (48, 64), (700, 716), (1072, 1097), (2144, 2160)] + wins8)
     o = OracleRenderer(path)
     o.set_row_windows(wins)
     want = o.update_and_render(W, H, inp)
@@ -229,6 +243,10 @@ def test_stress_1m_4k_rows_match_oracle(gpu_renderer, tmp_path):
     for y0 in (48, 1072):
         lr0 = (y0 // 16 // 8) * 16
         assert np.array_equal(part[lr0:lr0 + 16], want[y0:y0 + 16]), f'part 3 rows {y0}..{y0 + 15}'
+    for y0, y1 in wins8:
+        b = y0 // 135
+        p, lr0 = b % 8, (b // 8) * 135 + (y0 - 135 * b)
+        assert np.array_equal(parts8[p][lr0:lr0 + (y1 - y0)], want[y0:y1]), f'8-way part {p} rows {y0}..{y1 - 1}'
 
 
 @pytest.mark.parametrize('band,nparts', [(16, 2), (16, 3), (5, 2), (7, 4)])
