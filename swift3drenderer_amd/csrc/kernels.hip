@@ -1708,12 +1708,18 @@ S3R_HD float ooz_bound(const TriSetup &t) {
     return is_finite(b) && rmax > 0.0f && asum > 0.0f ? b : __builtin_inff();
 }
 
+// The live slot's raster record, stored non-temporal: the records (~10 M x 64 B on the stress
+// scene) stream out past the setup's index / vertex loads instead of occupying L2 until the raster
+// reads them.  Stress scene, one MI355X, same box (profiles/r05_ntrec_ab.txt): setup 608-610 ->
+// 577 us serialised, part 0 of 8 5 829-5 932 -> 6 283 fps, whole frame 979-993 -> 1 007 fps; the
+// bin entries stored the same way measured slower (624 us: the raster reads them back soon).
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot, uint32_t zb) {
-    float4 *q = reinterpret_cast<float4 *>(r);
-    reinterpret_cast<uint4 *>(r)[0] = make_uint4(t.xmin | (t.xmax << 16), t.ymin | (t.ymax << 16), slot, zb);
-    q[1] = make_float4(t.ws[0], t.ws[1], t.ws[2], t.dx[0]);
-    q[2] = make_float4(t.dx[1], t.dx[2], t.dy[0], t.dy[1]);
-    q[3] = make_float4(t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]);
+    nt_f4 *q = reinterpret_cast<nt_f4 *>(r);
+    __builtin_nontemporal_store((nt_f4){u2f(t.xmin | (t.xmax << 16)), u2f(t.ymin | (t.ymax << 16)), u2f(slot), u2f(zb)}, q);
+    __builtin_nontemporal_store((nt_f4){t.ws[0], t.ws[1], t.ws[2], t.dx[0]}, q + 1);
+    __builtin_nontemporal_store((nt_f4){t.dx[1], t.dx[2], t.dy[0], t.dy[1]}, q + 2);
+    __builtin_nontemporal_store((nt_f4){t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]}, q + 3);
 }
 
 // Vertex stage (render.cpp:285-289 as a pass over the vertex stream, north_star's "vertex-stage
@@ -1859,9 +1865,11 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
             bx = bt;
             by = ts.ymin | (ts.ymax << 16);
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 32)
-            if (slot == 0xFFFFFFFFu)                    // ablation: no raster record written
-#endif
+            // ablation (wrong pixels, bounded work): only the record's first 16 B (box, slot, bound)
+            reinterpret_cast<uint4 *>(recs + slot)[0] = make_uint4(ts.xmin | (ts.xmax << 16), ts.ymin | (ts.ymax << 16), slot, zb);
+#else
             write_rec(recs + slot, ts, slot, zb);
+#endif
         }
     }
     if (tbin) {
