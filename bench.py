@@ -77,6 +77,9 @@ def parse(argv=None):
     p.add_argument('--rank-devices', default=None,
                    help='comma-separated GPU of each rank in the ranks leg (default: LOCAL_RANK); repeated '
                         'ids rehearse ranks on one GPU and then need --gather-backend gloo')
+    p.add_argument('--ranks-extra', default=None,
+                   help='further WxH frames for the ranks leg, comma-separated (default with N > 1: 7680x4320, '
+                        'BASELINE config 4 -- the 8-GPU row-strip + RCCL gather config; "none": only the main frame)')
     p.add_argument('--gather-backend', default='nccl', choices=('nccl', 'gloo'),
                    help='the ranks leg\'s gather: nccl (RCCL over xGMI) or gloo (a rehearsal through host copies)')
     return p.parse_args(argv)
@@ -212,10 +215,15 @@ def main(argv=None):
         result = run_rank0(a, N, np, torch)
     barrier()
     if ranks_on:
-        rl = run_ranks_leg(a, rank, N, np, torch, dist,
-                           result['device_fps'] if rank == 0 and result else None)
-        if rank == 0:
-            result['ranks'] = rl
+        frames = [(a.width, a.height)]
+        extra = a.ranks_extra if a.ranks_extra is not None else ('7680x4320' if world > 1 else 'none')
+        if extra != 'none':
+            frames += [tuple(int(v) for v in f.split('x')) for f in extra.split(',') if f]
+        for k, (w, h) in enumerate(frames):
+            fps1 = result['device_fps'] if rank == 0 and result and k == 0 else None
+            rl = run_ranks_leg(a, rank, N, np, torch, dist, w, h, fps1)
+            if rank == 0:
+                result['ranks' if k == 0 else f'ranks_{w}x{h}'] = rl
     if rank == 0:
         print(json.dumps(result), flush=True)
     barrier()
@@ -279,8 +287,13 @@ def ranks_leg(render_part, render_whole, sync, gather, barrier, allgather_f, W, 
     return {'device_s': dev_times, 'gathered_s': gat_times, 'gathered_equals_whole': same}
 
 
-def run_ranks_leg(a, rank, N, np, torch, dist, device_fps_1):
-    """The ranks leg on this rank: its own GPU, its own library state, the part it owns."""
+_GROUPS = {}
+
+
+def run_ranks_leg(a, rank, N, np, torch, dist, W, H, device_fps_1):
+    """The ranks leg on this rank for a W x H frame: its own GPU, its own library state, the part it
+    owns.  device_fps_1 (rank 0): the whole frame's device-resident rate on one GPU; None: rank 0
+    measures it here first, the same way (frames pipelined into HBM), while the others wait."""
     from swift3drenderer_amd import poses, scene
     from swift3drenderer_amd.abi import Input
     from swift3drenderer_amd.multi import BandGather, band_rows
@@ -292,15 +305,32 @@ def run_ranks_leg(a, rank, N, np, torch, dist, device_fps_1):
     tmp = tempfile.mkdtemp(prefix=f's3r_rank{rank}_')
     data_path = os.path.join(tmp, f'{a.scene}.bin')
     scene.write_named(a.scene, data_path)
-    W, H = a.width, a.height
+    script, hold_in = poses.script(a.pose), Input.of(poses.hold(a.pose))
+    st = torch.cuda.current_stream(dev)
+    steps = max(a.steps, MIN_TIMED)
+    if rank == 0 and not device_fps_1:
+        r1 = Renderer(data_path, device=dev_id)
+        frame = torch.empty((H, W), dtype=torch.int32, device=dev)
+        for t in script:
+            r1.render_bands(t, W, H, H, 1, 0, frame.data_ptr(), st.cuda_stream)
+        for _ in range(max(a.warmup, MIN_WARMUP)):
+            r1.render_bands(hold_in, W, H, H, 1, 0, frame.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r1.render_bands(hold_in, W, H, H, 1, 0, frame.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        device_fps_1 = steps / (time.perf_counter() - t0)
+        del frame
+    dist.barrier()
     r = Renderer(data_path, device=dev_id)
     B = a.band or r.frame_band(H, N)
     if N == 1:
         B = H
-    script, hold_in = poses.script(a.pose), Input.of(poses.hold(a.pose))
-    st = torch.cuda.current_stream(dev)
     nccl = a.gather_backend == 'nccl'
-    group = dist.new_group(backend='nccl') if nccl else None
+    if nccl and 'nccl' not in _GROUPS:
+        _GROUPS['nccl'] = dist.new_group(backend='nccl')      # (one communicator for every frame size)
+    group = _GROUPS.get('nccl') if nccl else None
     bg = BandGather(W, H, B, N, rank, dev)
     if not nccl:
         cpu = BandGather(W, H, B, N, rank, torch.device('cpu'))
@@ -333,16 +363,17 @@ def run_ranks_leg(a, rank, N, np, torch, dist, device_fps_1):
         dist.all_gather_object(out, float(x))
         return out
 
-    steps = max(a.steps, MIN_TIMED)
     res = ranks_leg(render_part, whole, lambda: torch.cuda.synchronize(dev), gather, dist.barrier, allgather_f,
                     W, H, B, N, rank, steps, max(a.warmup, MIN_WARMUP))
     r.shutdown()
     shutil.rmtree(tmp, ignore_errors=True)
     if rank != 0:
         return None
-    return ranks_summary(res, W, H, B, N, steps, device_fps_1, [band_rows(H, B, N, p) for p in range(N)],
+    out = ranks_summary(res, W, H, B, N, steps, device_fps_1, [band_rows(H, B, N, p) for p in range(N)],
                          'rccl (torch.distributed nccl) gather + s3r_deinterleave_bands' if nccl else
                          'gloo gather through host copies (rehearsal) + index_select')
+    out['frame'] = f'{a.scene}/{a.pose}/{W}x{H}'
+    return out
 
 
 def ranks_summary(res, W, H, B, N, steps, device_fps_1, rows, gather_desc):

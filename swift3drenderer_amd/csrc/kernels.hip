@@ -324,9 +324,6 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #ifndef S3R_PX
 #define S3R_PX 1
 #endif
-#ifndef S3R_TWO_PIECE
-#define S3R_TWO_PIECE 1                // batch 0: chunks crossing one binade edge as two linear pieces
-#endif
 #ifndef S3R_LINE_STORES
 #define S3R_LINE_STORES 1              // HOSTW: wave stores on the caller buffer's 64-B line grid
 #endif
@@ -358,7 +355,6 @@ static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
 // kPairWords uint4): a tuning build with fewer tables must still leave room for them.
 static_assert(sizeof(((FragShared *)nullptr)->tab4) >= 64u * 8u * sizeof(uint4),
               "pair staging (kPairMax * kPairWords uint4) must fit in tab4");
-constexpr uint32_t kNoTable = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask, uint32_t lane) {
     return (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
@@ -904,136 +900,73 @@ S3R_CALLEE uint32_t shade(const TriSetup *__restrict__ tp, float w0, float w1, f
 #endif
 }
 
-// Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle.
-// Batch 0 also knows two-piece chunks (two = true): pixels k <= kb are c + k*del, pixels k > kb are
-// c2 + (k - kb - 1)*del2 (a binade edge crossed inside the chunk).
+// Per-lane values of one batch: lane 3t+c holds component c of the batch's t-th triangle; c is the
+// exact value at pixel k0 of the component's walk (render.cpp:374), m the triangle's pixels in the chunk.
 struct BatchLanes {
-    bool ov = false, lin = false, neg = false, two = false;
-    float c = 0.0f, d = 0.0f, del = 0.0f, rz = 0.0f, c2 = 0.0f, del2 = 0.0f;
-    uint32_t k0 = 0, m = 0, xmax = 0, slot = 0, kb = 0;
-};
-struct BatchMasks {
-    uint64_t ovm, negm, irrm, twom;
-    uint32_t tix;
+    bool ov = false;
+    float c = 0.0f, d = 0.0f, rz = 0.0f;
+    uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
 };
 
-// Pruning and exact tables for one batch: a triangle with a component negative over the whole chunk
-// covers none of it; a non-linear component gets a 64-entry table filled by the reference's own
-// sequential loop (render.cpp:374).  `last` = the component's exact value at the chunk's last pixel
-// (or at its first, for a pruned non-linear component), the walk state for the next chunk.
-__device__ __forceinline__ void batch_resolve(BatchLanes &v, uint32_t tl, uint32_t lane, float (*tab)[kChunk],
-                                              BatchMasks &bm, float &last
-#ifdef S3R_STATS
-                                              , uint32_t *p_chunk
-#endif
-) {
-    bm.ovm = __ballot(v.ov && (lane - 3u * tl) == 0u);
-    bm.tix = kNoTable;
-    last = v.two ? v.c2 + (float)(v.m - 2u - v.kb) * v.del2 : v.c + (float)(v.m - 1u) * v.del;
-    if (bm.ovm == 0) { bm.negm = bm.irrm = bm.twom = 0; return; }
-    bm.negm = __ballot(v.neg);
-    bm.twom = __ballot(v.ov && v.two);
-    bm.irrm = __ballot(v.ov && !v.lin && !v.two && !((bm.negm >> (3u * tl)) & 7ull));
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 2048)
-    if (false) {                              // ablation: no tables, no pruning walks
-#else
-    if (v.ov && !v.lin && !v.two) {
-#endif
-        if ((bm.negm >> (3u * tl)) & 7ull) {
-            last = v.c;                       // pruned: keep the state at the chunk start
-            v.m = 1u;
-        } else {
-            const uint32_t r = lane_prefix(bm.irrm, lane);
-            if (r < kTables) {
-                // the reference's own sequential adds (render.cpp:374), all kChunk of them, unrolled
-                // and stored four at a time (entries past m are never read); `last` = entry m - 1
-                float w = v.c;
-                float4 *tb4 = reinterpret_cast<float4 *>(tab[r]);
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 8192)
-                tb4[0] = make_float4(w, w, w, w);     // ablation: no sequential fill
-#else
-#pragma unroll
-                for (uint32_t k4 = 0; k4 < kChunk / 4u; k4++) {
-                    const float a1 = w + v.d, a2 = a1 + v.d, a3 = a2 + v.d;
-                    tb4[k4] = make_float4(w, a1, a2, a3);
-                    w = a3 + v.d;
-                }
-#endif
-                last = tab[r][v.m - 1u];
-                bm.tix = r;
-            } else {
-                last = walk(v.c, v.d, v.m - 1u S3R_IT(p_chunk));
+// One chunk of one batch.  Every (triangle, component) that overlaps the chunk gets the chunk's 64
+// exact values by the reference's own sequential adds (render.cpp:374, w += dx) in an LDS table --
+// every lane of the wave the same instruction stream: no per-lane linear-run classification, no
+// exact_walk inside a row (round 5; the linear-run design it replaces classified each chunk per lane,
+// jumped inside binades and filled tables only for irregular chunks: 56.8 -> 52.0 us per 4K launch,
+// 31.0 -> 26.6 M VALU and 16.3 -> 12.3 M SALU wave-instructions, profiles/r05_fragment_ab.txt).  Then
+// lanes act as pixels: edge test, 1/z and the strict '>' depth test in registers, reading the tables.
+// v.c is the exact value at pixel v.k0; `last` returns the value at v.k0 + v.m - 1, the walk state
+// of the next chunk.  Tables hold kTables components = kTables / 3 triangles: a chunk met by more runs
+// in groups, in list (slot) order -- the reference's order, which decides depth ties.
+static_assert(kPX == 1u && kTables % 3u == 0u, "one pixel per lane, whole triangles per table group");
+__device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane, float (*tab)[kChunk], uint32_t xl,
+                                             float (&depth)[kPX], int (&win)[kPX], float (&bw0)[kPX],
+                                             float (&bw1)[kPX], float (&bw2)[kPX], float &last) {
+    last = v.c;
+    const uint64_t ovl = __ballot(v.ov);
+    if (ovl == 0) return;
+    const uint32_t r = lane_prefix(ovl, lane), nov = (uint32_t)__builtin_popcountll(ovl);
+    for (uint32_t g0 = 0; g0 < nov; g0 += kTables) {                    // wave-uniform
+        const bool mine = v.ov && r >= g0 && r < g0 + kTables;
+        const uint32_t ti = r - g0;
+        bool neg = false;
+        if (mine) {
+            float w = v.c;
+            float4 *tb4 = reinterpret_cast<float4 *>(tab[ti]);
+#pragma unroll 4                                   // (fully unrolled, the kernel spills 68 VGPRs)
+            for (uint32_t k4 = 0; k4 < kChunk / 4u; k4++) {
+                const float a1 = w + v.d, a2 = a1 + v.d, a3 = a2 + v.d;
+                tb4[k4] = make_float4(w, a1, a2, a3);
+                w = a3 + v.d;
+                __builtin_amdgcn_sched_barrier(0);   // store as it goes: the chain's values must not pile up in VGPRs
             }
-            v.neg = v.c < 0.0f && last < 0.0f;
         }
+        wave_sync();
+        if (mine) {
+            last = tab[ti][v.m - 1u];
+            neg = v.c < 0.0f && last < 0.0f;                               // monotone walk: all < 0
+        }
+        const uint64_t negm = __ballot(neg);
+        const uint64_t gm = __ballot(mine);
+        uint64_t live = gm & ~(negm | (negm >> 1) | (negm >> 2)) & 0x9249249249249249ull;
+        while (live) {
+            const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
+            live &= live - 1;
+            const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0), t0 = rdl(ti, l0);
+            const float r0 = rdl(v.rz, l0), r1 = rdl(v.rz, l0 + 1u), r2 = rdl(v.rz, l0 + 2u);
+            const int tslot = (int)rdl(v.slot, l0);
+            if (xl < tk0 || xl > txmax) continue;
+            const uint32_t off = xl - tk0;
+            const float a0 = tab[t0][off], a1 = tab[t0 + 1u][off], a2 = tab[t0 + 2u][off];
+            if (a0 >= 0 && a1 >= 0 && a2 >= 0) {                               // :362
+                const float ooz = (r0 * a0 + r1 * a1) + r2 * a2;                 // :363
+                if (ooz > depth[0]) {                                             // :364
+                    depth[0] = ooz; win[0] = tslot; bw0[0] = a0; bw1[0] = a1; bw2[0] = a2;
+                }
+            }
+        }
+        wave_sync();                                                        // before the next group's fill
     }
-    bm.negm = __ballot(v.neg);
-    if (bm.irrm) wave_sync();
-}
-
-// Lanes as pixels: triangles in slot order (bit 3t of `live`); (triangle, component) values are
-// broadcast from their lanes with v_readlane.  Edge test, 1/z, strict '>' depth test in registers.
-__device__ __forceinline__ void pixel_phase(const BatchLanes &v, const BatchMasks &bm, uint32_t xl, float (*tab)[kChunk],
-                                            float (&depth)[kPX], int (&win)[kPX], float (&bw0)[kPX],
-                                            float (&bw1)[kPX], float (&bw2)[kPX]
-#ifdef S3R_STATS
-                                            , uint32_t *p_pix, uint32_t *p_tests
-#endif
-) {
-    const uint64_t neg3 = bm.negm | (bm.negm >> 1) | (bm.negm >> 2);
-    uint64_t live = bm.ovm & ~neg3 & 0x9249249249249249ull;   // bits 0, 3, 6, ...
-    while (live) {
-        const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
-        live &= live - 1;
-        const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0);
-        float cv[3], dv[3], r[3];
-        uint32_t lmask = 0, tmask = 0;
-#pragma unroll
-        for (uint32_t cc = 0; cc < 3; cc++) {
-            const uint32_t l = l0 + cc;
-            cv[cc] = rdl(v.c, l);
-            dv[cc] = rdl(v.del, l);
-            r[cc] = rdl(v.rz, l);
-            lmask |= (uint32_t)((bm.irrm >> l) & 1ull) << cc;
-            tmask |= (uint32_t)((bm.twom >> l) & 1ull) << cc;
-        }
-        const int tslot = (int)rdl(v.slot, l0);
-#pragma unroll
-        for (uint32_t p = 0; p < kPX; p++) {
-            const uint32_t x = xl + 64u * p;
-            if (x < tk0 || x > txmax) continue;
-#ifdef S3R_STATS
-            (*p_tests)++;
-#endif
-            const uint32_t off = x - tk0;
-            const float fo = (float)off;
-            float a[3];
-#pragma unroll
-            for (uint32_t cc = 0; cc < 3; cc++) {
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 2)
-                a[cc] = cv[cc] + fo * dv[cc];
-#else
-                if ((tmask >> cc) & 1u) {
-                    const uint32_t l = l0 + cc, kb = rdl(v.kb, l);           // two linear pieces
-                    a[cc] = off <= kb ? cv[cc] + fo * dv[cc] : rdl(v.c2, l) + (float)(off - kb - 1u) * rdl(v.del2, l);
-                } else if (!((lmask >> cc) & 1u)) {
-                    a[cc] = cv[cc] + fo * dv[cc];                      // linear chunk (or pruned: unused)
-                } else {
-                    const uint32_t l = l0 + cc;
-                    const uint32_t ti = rdl(bm.tix, l);
-                    a[cc] = ti != kNoTable ? tab[ti][off] : walk(cv[cc], rdl(v.d, l), off S3R_IT(p_pix));
-                }
-#endif
-            }
-            if (a[0] >= 0 && a[1] >= 0 && a[2] >= 0) {                        // :362
-                const float ooz = (r[0] * a[0] + r[1] * a[1]) + r[2] * a[2];  // :363
-                if (ooz > depth[p]) {                                           // :364
-                    depth[p] = ooz; win[p] = tslot; bw0[p] = a[0]; bw1[p] = a[1]; bw2[p] = a[2];
-                }
-            }
-        }
-    }
-    if (bm.irrm) wave_sync();
 }
 
 // A workgroup = 4 waves = 4 consecutive local rows x one segment of SEGCH 64-pixel chunks.  The
@@ -1180,11 +1113,11 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     S3R_WGT(2);
 
     // ---- batch 0 (the first kTPB listed triangles: nearly every row has no more) keeps its
-    // constants, walk state and current linear run in registers
+    // constants and walk state in registers
     const bool reg0 = !overflow && row_ok && n0 > 0;
     bool r0_in = false;
-    float r0_d = 0.0f, r0_rz = 0.0f, r0_sc = 0.0f, r0_base = 0.0f, r0_del = 0.0f;
-    uint32_t r0_xmin = 1u, r0_xmax = 0u, r0_slot = 0u, r0_sk = 0u, r0_k = 1u, r0_end = 0u;
+    float r0_d = 0.0f, r0_rz = 0.0f, r0_sc = 0.0f;
+    uint32_t r0_xmin = 1u, r0_xmax = 0u, r0_slot = 0u, r0_sk = 0u;
     if (reg0 && lane < 63 && tl < n0) {
         const Entry &e = sh.ent[tl];
         r0_in = y >= e.ymin && y <= e.ymax;
@@ -1233,86 +1166,24 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         for (uint32_t p = 0; p < kPX; p++) { depth[p] = 0.0f; bw0[p] = bw1[p] = bw2[p] = 0.0f; win[p] = -1; }
 
         S3R_WGC_MARK();
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 8)
-        if (false) {
-#else
         if (reg0) {
-#endif
             BatchLanes v;
             if (r0_in && r0_xmin <= cx1 && r0_xmax >= cx0) {
                 v.ov = true;
                 v.d = r0_d; v.rz = r0_rz; v.xmax = r0_xmax; v.slot = r0_slot;
                 v.k0 = max(cx0, r0_xmin);
-                const uint32_t kend = min(cx1, r0_xmax);
-                v.m = kend - v.k0 + 1u;
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 1024)
-                if (true) {                          // ablation: every chunk inside the linear run
-                    if (r0_end == 0u) { r0_base = r0_sc; r0_k = r0_sk; r0_del = r0_d; r0_end = 0xFFFFFFFFu; }
-#else
-                if (v.k0 >= r0_k && kend <= r0_end) {
-#endif
-                    // inside the current linear run: exact c + k*delta, no walking, no test
-                    v.c = r0_base + (float)(v.k0 - r0_k) * r0_del;
-                    v.del = r0_del;
-                    v.lin = true;
-                } else {
-                    S3R_WGN(0, 1u);
-                    float j;
-                    if (v.k0 >= r0_k && v.k0 <= r0_end) {
-                        // the current run ends inside this chunk: its remaining j regular steps
-                        v.c = r0_base + (float)(v.k0 - r0_k) * r0_del;
-                        v.del = r0_del;
-                        j = (float)(r0_end - v.k0);
-                    } else {
-                        // state = exact value at pixel r0_sk: contiguous chunks need 0 or 1 step
-                        v.c = v.k0 == r0_sk ? r0_sc
-                                            : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
-                        j = linear_run(v.c, v.d, &v.del);
-                        if (j >= 1.0f) {
-                            r0_base = v.c; r0_k = v.k0; r0_del = v.del;
-                            r0_end = j >= 65536.0f ? 0xFFFFFFFFu : v.k0 + (uint32_t)j;
-                        } else {
-                            r0_k = 1u; r0_end = 0u;
-                        }
-                    }
-                    v.lin = j >= (float)(v.m - 1u);
-#if S3R_TWO_PIECE && !(defined(S3R_ABLATE) && (S3R_ABLATE & 4096))
-                    if (!v.lin) {
-                        // a binade edge inside the chunk: pixels 0..j are c + k*delta (exact), pixel
-                        // j + 1 is the reference's one add across the edge, and from there the next
-                        // binade's run -- two linear pieces when that run reaches the chunk end
-                        const uint32_t ji = (uint32_t)j;
-                        const float c2 = (v.c + (float)ji * v.del) + v.d;            // render.cpp:374
-                        float d2;
-                        const float j2 = linear_run(c2, v.d, &d2);
-                        if (j2 >= (float)(v.m - 2u - ji)) {
-                            v.two = true; v.c2 = c2; v.del2 = d2; v.kb = ji;
-                            r0_base = c2; r0_k = v.k0 + ji + 1u; r0_del = d2;
-                            r0_end = j2 >= 65536.0f ? 0xFFFFFFFFu : r0_k + (uint32_t)j2;
-                        }
-                    }
-#endif
-                }
-                if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;   // monotone walk
-                else if (v.two) v.neg = v.c < 0.0f && v.c2 + (float)(v.m - 2u - v.kb) * v.del2 < 0.0f;
+                v.m = min(cx1, r0_xmax) - v.k0 + 1u;
+                // the state is the exact value at pixel r0_sk <= k0: the chunk before's last pixel (one
+                // add), or for a triangle's first chunk the bin's start point (a jump)
+                v.c = v.k0 == r0_sk ? r0_sc
+                                    : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
             }
-            BatchMasks bm;
             float last;
-            batch_resolve(v, tl, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), bm, last S3R_IT(p_chunk));
+            alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last);
             if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
-            S3R_WGN(1, bm.irrm ? 1u : 0u);
-            S3R_WGN(2, (uint32_t)__builtin_popcountll(bm.ovm & ~(bm.negm | (bm.negm >> 1) | (bm.negm >> 2)) & 0x9249249249249249ull));
-            if (bm.ovm) {
 #ifdef S3R_STATS
-                st_batches++;
-                st_irr += (v.ov && !v.lin) ? 1u : 0u;
+            st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
 #endif
-#if defined(S3R_ABLATE) && (S3R_ABLATE & 4)
-                if (x == 0xFFFFFFFFu) win[0] = (int)(bm.ovm ^ bm.negm);   // keep the phase alive, skip pixels
-#else
-                pixel_phase(v, bm, x, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
-#endif
-            }
         }
 
         S3R_WGC_ADD(0);
@@ -1349,20 +1220,14 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                             const float c0v = rowtab[(((size_t)e.slot * rows_local + lr) * nst + j) * 4 + comp];
                             v.c = walk(c0v, v.d, v.k0 - k S3R_IT(p_chunk));
                         }
-                        v.lin = chunk_linear(v.c, v.d, v.m, &v.del);
-                        if (v.lin) v.neg = v.c < 0.0f && v.c + (float)(v.m - 1u) * v.del < 0.0f;
                     }
                 }
-                BatchMasks bm;
                 float last;
-                batch_resolve(v, tl, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), bm, last S3R_IT(p_chunk));
+                alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last);
                 if (v.ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = v.k0 + v.m - 1u; }
-                if (bm.ovm == 0) continue;
 #ifdef S3R_STATS
-                st_batches++;
-                st_irr += (v.ov && !v.lin) ? 1u : 0u;
+                st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
 #endif
-                pixel_phase(v, bm, x, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), depth, win, bw0, bw1, bw2 S3R_IT(p_pix) S3R_IT(&st_tests));
             }
             if (!overflow || cursor >= nslots) break;
         }

@@ -6,6 +6,6 @@
 for v in "" 1 5 13 29 157; do
   lib=swift3drenderer_amd/librender.so; [ -n "$v" ] && lib=build/librender_ablate$v.so
   for pose in P_over P_id; do
-    S3R_LIB=$lib timeout -k 10 120 python bench.py --pose $pose --steps 100 --warmup 10 --no-cpu-baseline --no-e2e "$@" 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('ablate=${v:-0}', '$pose', 'frag_ms', d['fragment_kernel_ms'], 'fps', d['value'])" || exit 1
+    S3R_LIB=$lib timeout -k 10 120 python bench.py --pose $pose --steps 100 --warmup 10 --no-cpu-baseline "$@" 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('ablate=${v:-0}', '$pose', 'frag_ms', d['fragment_kernel_ms'], 'fps', d['value'])" || exit 1
   done
 done

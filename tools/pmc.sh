@@ -6,7 +6,7 @@
 #   PMC_CMD="python3 tools/overhead_probe.py --scene icosa-stress --nparts 8 --steps 10 --data /tmp/s.bin"
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
-ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline --no-e2e}
+ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOTDIR=$(pwd)

@@ -24,3 +24,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$ROOTDIR/$OUT/pmc$i" -o run -- python3 bench.py $BARGS > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -5 "$OUT/pmc$i.log"; exit 1; }
 done
 python3 tools/pmc_summary.py "$OUT" --last "$STEPS" --workload "$WORKLOAD"
+# the per-dispatch CSVs are large (the box returns at most 64 MiB of gpurun_out/): keep the stats and
+# the summaries made from them
+find "$OUT" \( -name '*kernel_trace.csv' -o -name '*counter_collection.csv' -o -name '*agent_info.csv' \) -delete

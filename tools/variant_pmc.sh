@@ -7,7 +7,7 @@ OUT=${1:-gpurun_out/vpmc}; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 ROOTDIR=$(pwd)
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-e2e $BENCH_ARGS"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline $BENCH_ARGS"
 for tag in "$@"; do
   lib=build/librender_$tag.so; [ "$tag" = prod ] && lib=swift3drenderer_amd/librender.so
   i=0
@@ -39,3 +39,4 @@ print('counter'.ljust(26) + ''.join(t.rjust(14) for t in tags))
 for c in cs:
     print(c.ljust(26) + ''.join(f'{rows[t].get(c, float("nan")):14.4g}' for t in tags))
 EOF
+find "$OUT" \( -name '*counter_collection.csv' -o -name '*agent_info.csv' \) -delete
