@@ -324,6 +324,12 @@ constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x
 #ifndef S3R_PX
 #define S3R_PX 1
 #endif
+#ifndef S3R_WORK_SKY
+#define S3R_WORK_SKY 8                 // a sky bin's work units (its fill of the background)
+#endif
+#ifndef S3R_ORDER_WALL
+#define S3R_ORDER_WALL 0               // 1: bins ordered by their measured wall time (rounds 3-4)
+#endif
 #ifndef S3R_LINE_STORES
 #define S3R_LINE_STORES 1              // HOSTW: wave stores on the caller buffer's 64-B line grid
 #endif
@@ -349,6 +355,7 @@ struct FragShared {
     uint32_t cnt, next;
     uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
     uint32_t bgm[kWaves];                // host fill: per wave (row), its chunks left to the host
+    uint32_t wwork[kWaves];              // per wave: its work units (the bin's cost, order_bins)
 };
 static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
 // k_fragment stages a bin's pair records in tab4 before the chunk loop (s3r_kernels.h kPairMax x
@@ -474,12 +481,12 @@ uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
 // Longest-first order of the fragment bins (workgroups): a fragment launch is several rounds of
 // resident workgroups whose costs differ ~8x (textured floor rows vs sky), and the launch order
 // (top-down) can leave the costliest rows for the last round.  One workgroup counting-sorts the bins
-// by their cost when the buffer set was last used (k_fragment's order[n + bin], 10 ns ticks; stale
+// by their cost when the buffer set was last used (k_fragment's order[n + bin], work units; stale
 // values from another frame size are only hints; no fragment launch of the set runs meanwhile, so
 // both passes read the same values) into kOrderBuckets quarter-octave buckets,
 // costliest first; perm is always a permutation of [0, n).
 constexpr uint32_t kOrderBuckets = 32;
-// bucket of a cost: a quarter octave each from 2^6 ticks (0.64 us) -- no max pass over the costs
+// bucket of a cost: a quarter octave each from 2^6 units (a sky bin: kWorkSky) -- no max pass over the costs
 __device__ __forceinline__ uint32_t order_bucket(uint32_t c) {
     const float l = __log2f((float)max(c, 64u)) * 4.0f - 24.0f;
     return min((uint32_t)l, kOrderBuckets - 1u);
@@ -908,6 +915,16 @@ struct BatchLanes {
     uint32_t k0 = 0, m = 0, xmax = 0, slot = 0;
 };
 
+// Work units (~8 VALU instructions each) a wave counts for the longest-first order of the next
+// frames (order_bins): a table group's fill, one live triangle's pixel test, one shading round of a
+// textured / coloured winner (a non-waterfall chunk with any winner: kWorkShade), a chunk.  Round 5:
+// the wall time of a bin, used before, depends on its co-resident workgroups -- a bin that ran in
+// the launch's sparse tail measures short and stays in the tail -- so the order did not converge
+// to the heaviest bins first (4K P_over, per-workgroup timeline: span 54.8 us with the wall-time
+// order, 55.6 in launch order; list scheduling of the measured durations costliest first: 44.0).
+constexpr uint32_t kWorkFill = 12, kWorkTest = 4, kWorkTexture = 32, kWorkColour = 20, kWorkShade = 24,
+                   kWorkChunk = 2, kWorkSky = S3R_WORK_SKY;
+
 // One chunk of one batch.  Every (triangle, component) that overlaps the chunk gets the chunk's 64
 // exact values by the reference's own sequential adds (render.cpp:374, w += dx) in an LDS table --
 // every lane of the wave the same instruction stream: no per-lane linear-run classification, no
@@ -921,12 +938,13 @@ struct BatchLanes {
 static_assert(kPX == 1u && kTables % 3u == 0u, "one pixel per lane, whole triangles per table group");
 __device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane, float (*tab)[kChunk], uint32_t xl,
                                              float (&depth)[kPX], int (&win)[kPX], float (&bw0)[kPX],
-                                             float (&bw1)[kPX], float (&bw2)[kPX], float &last) {
+                                             float (&bw1)[kPX], float (&bw2)[kPX], float &last, uint32_t &wk) {
     last = v.c;
     const uint64_t ovl = __ballot(v.ov);
     if (ovl == 0) return;
     const uint32_t r = lane_prefix(ovl, lane), nov = (uint32_t)__builtin_popcountll(ovl);
     for (uint32_t g0 = 0; g0 < nov; g0 += kTables) {                    // wave-uniform
+        wk += kWorkFill;
         const bool mine = v.ov && r >= g0 && r < g0 + kTables;
         const uint32_t ti = r - g0;
         bool neg = false;
@@ -952,6 +970,7 @@ __device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane,
         while (live) {
             const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
             live &= live - 1;
+            wk += kWorkTest;
             const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0), t0 = rdl(ti, l0);
             const float r0 = rdl(v.rz, l0), r1 = rdl(v.rz, l0 + 1u), r2 = rdl(v.rz, l0 + 2u);
             const int tslot = (int)rdl(v.slot, l0);
@@ -1010,7 +1029,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     // k_geometry) or the launch order; either way a permutation of the bins, so the pixels do not
     // depend on it
     const uint32_t bid = order ? order[blockIdx.x] : blockIdx.x;
-    if (order && threadIdx.x == 0) sh.t_start = (uint32_t)wall_clock64();   // in LDS: no live registers
+    if (S3R_ORDER_WALL && order && threadIdx.x == 0) sh.t_start = (uint32_t)wall_clock64();   // in LDS: no live registers
     const uint32_t blk = bid / segs, seg = bid - blk * segs;
     const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
@@ -1069,7 +1088,8 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
             }
         }
         S3R_WGT(3);
-        if (order && threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
+        if (order && threadIdx.x == 0)
+            order[gridDim.x + bid] = S3R_ORDER_WALL ? (uint32_t)wall_clock64() - sh.t_start : kWorkSky;
         return;
     }
     if (npairs > kPairMax) {
@@ -1154,10 +1174,12 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         carry = rot;
     };
     S3R_WGC_DECL;
+    uint32_t wk = 0;                     // this wave's work units (kWorkFill ...), wave-uniform
     for (uint32_t q = 0; q < SEGCH; q++) {
         const uint32_t cx0 = xs + kChunk * q;
         if (cx0 > xe) break;
         cx_next = cx0 + kChunk;
+        wk += kWorkChunk;
         const uint32_t cx1 = min(cx0 + kChunk - 1u, xe);
         const uint32_t x = cx0 + lane;                     // this lane's pixels: x + 64 p, p < kPX
         float depth[kPX], bw0[kPX], bw1[kPX], bw2[kPX];
@@ -1179,7 +1201,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                     : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
             }
             float last;
-            alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last);
+            alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
             if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
 #ifdef S3R_STATS
             st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
@@ -1223,7 +1245,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                     }
                 }
                 float last;
-                alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last);
+                alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
                 if (v.ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = v.k0 + v.m - 1u; }
 #ifdef S3R_STATS
                 st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
@@ -1263,6 +1285,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
 #else
             if (!WF) {
                 const bool act = row_ok && xp <= xe;
+                if (order && __ballot(act && win[p] >= 0)) wk += kWorkShade;
                 uint32_t px = kNoPixel;
                 if (act) px = win[p] < 0 ? kBackground : shade(tris + win[p], bw0[p], bw1[p], bw2[p], depth[p], tex, ntex);
                 if (HOSTW) {
@@ -1287,6 +1310,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                     const float4 c0 = q[6], c1 = q[7], c2 = q[8], n0 = q[9], n1 = q[10], n2 = q[11];
                     const float4 k0 = q[12], k1 = q[13], k2 = q[14];
                     const uint32_t kind = tp->kind, tex_base = tp->tex_base;
+                    wk += kind == kTexture ? kWorkTexture : kWorkColour;
                     const bool mine = act && wp == wu;
                     todo &= ~__ballot(mine);
                     if (mine)
@@ -1318,8 +1342,22 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         }
     }
     S3R_WGT(3);
-    // this bin's cost (wave 0's wall time, 10 ns ticks) for the buffer set's next order_bins
-    if (order && threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
+    // this bin's cost for the buffer set's next order_bins: its waves' work units (S3R_ORDER_WALL:
+    // wave 0's wall time, 10 ns ticks)
+    if (order) {
+        if (S3R_ORDER_WALL) {
+            if (threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
+        } else {
+            if (lane == 0) sh.wwork[wave] = wk;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t c = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < kWaves; w++) c += sh.wwork[w];
+                order[gridDim.x + bid] = c;
+            }
+        }
+    }
     S3R_WGC_STORE(n0);
 #ifdef S3R_STATS
     {
@@ -1394,9 +1432,9 @@ static_assert(sizeof(RasterRec) == 64, "RasterRec layout");
 // The corner's camera-space and raster position (render.cpp:286, :288).  The two projections share
 // one refined reciprocal of -cv.z where the trimmed division is exact (div_in_range, s3r_common.h);
 // z = (0 * factor) / nz + nz is nz itself unless nz == 0 (0 / 0: the reference's NaN).
-__device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint32_t vi, const Mat34 &m, float factor,
-                                            float half_w, float half_h, Vert &d) {
-    const F3 c = mat_mul(m, vtx[vi]);                                     // :286
+__device__ __forceinline__ void project_corner(float4 v, const Mat34 &m, float factor, float half_w, float half_h,
+                                               Vert &d) {
+    const F3 c = mat_mul(m, v);                                           // :286
     const float nz = -c.z;
     d.cv = c;
     const float px = c.x * factor, py = (-c.y) * factor;
@@ -1415,6 +1453,10 @@ __device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint
     float rz = nz;                                                          // (+-0) + nz == nz
     if (nz == 0.0f) rz = (0.0f * factor) / nz + nz;
     d.rv = mk3(qx + half_w, qy + half_h, rz);                               // :288
+}
+__device__ __forceinline__ void load_corner(const float4 *__restrict__ vtx, uint32_t vi, const Mat34 &m, float factor,
+                                            float half_w, float half_h, Vert &d) {
+    project_corner(vtx[vi], m, factor, half_w, half_h, d);
 }
 
 // Exact a / b for small operands by one float multiply (the integer division by a run-time divisor
@@ -1778,43 +1820,52 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     uint4 *const lv = live + 2ull * b0;
     uint32_t *const nlive = shard_ctr(ctr, 1, sh_id), *const nclip = shard_ctr(ctr, 2, sh_id);
     const float half_w = sw / 2, half_h = sh / 2;
-    // software pipeline over the loop's iterations: this iteration's slot and vertex indices were
-    // loaded during the previous one, the next iteration's are loaded during this one, and (with
-    // clusters) the cull's position for the one after that -- so an iteration waits for its corners
-    // only, not for the cmap -> slot -> index chain in front of them
+    // software pipeline over the loop's iterations, two deep: this iteration's corners (vertices, or
+    // the vertex stage's projected ones) were loaded during the previous iteration, the next one's
+    // corners and the one after's slot and vertex indices load during this one, and (with clusters) the
+    // cull's position for the iteration after that -- an iteration's loads are in flight while the
+    // iteration before sets up and bins its triangles, so a wave waits on no load chain
     const uint32_t step = per * 256u, jl = rank * 256u + threadIdx.x;
     auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : b0 + jj; };
-    uint32_t t_cur = 0, vi_cur[3] = {0, 0, 0}, q_next = 0;
+    const float4 *__restrict__ src = VS ? vrv : vtx;
+    uint32_t t_cur = 0, t_nxt = 0, vi_nxt[3] = {0, 0, 0}, q_next = 0;
+    float4 c_cur[3] = {make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0)};
     if (jl < n) {
         t_cur = slot_at(jl, CL ? cmap[b0 + jl] : 0u);
 #pragma unroll
-        for (int k = 0; k < 3; k++) vi_cur[k] = vidx[3 * t_cur + k];
+        for (int k = 0; k < 3; k++) c_cur[k] = src[vidx[3 * t_cur + k]];
     }
-    if (CL && jl + step < n) q_next = cmap[b0 + jl + step];
+    if (jl + step < n) {
+        t_nxt = slot_at(jl + step, CL ? cmap[b0 + jl + step] : 0u);
+#pragma unroll
+        for (int k = 0; k < 3; k++) vi_nxt[k] = vidx[3 * t_nxt + k];
+    }
+    if (CL && jl + 2u * step < n) q_next = cmap[b0 + jl + 2u * step];
     for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += step) {   // wave-uniform
         const uint32_t j = j0 + lane;
         Vert d[3];
         TriSetup ts;
         bool live_t = false, clip = false;
         const uint32_t t = t_cur;
+        const float4 c0 = c_cur[0], c1 = c_cur[1], c2 = c_cur[2];
+        if (j + step < n) {                                     // the next iteration's corners
+            t_cur = t_nxt;
+#pragma unroll
+            for (int k = 0; k < 3; k++) c_cur[k] = src[vi_nxt[k]];
+        }
+        if (j + 2u * step < n) {                                // the one after's slot and indices
+            t_nxt = slot_at(j + 2u * step, q_next);
+#pragma unroll
+            for (int k = 0; k < 3; k++) vi_nxt[k] = vidx[3 * t_nxt + k];
+        }
+        if (CL && j + 3u * step < n) q_next = cmap[b0 + j + 3u * step];
         if (j < n) {
+            const float4 cc[3] = {c0, c1, c2};
 #pragma unroll
             for (int k = 0; k < 3; k++) {
-                if (VS) {
-                    const float4 r = vrv[vi_cur[k]];                               // the vertex stage's rv
-                    d[k].rv = mk3(r.x, r.y, r.z);
-                } else {
-                    load_corner(vtx, vi_cur[k], m, factor, half_w, half_h, d[k]);
-                }
+                if (VS) d[k].rv = mk3(cc[k].x, cc[k].y, cc[k].z);                 // the vertex stage's rv
+                else project_corner(cc[k], m, factor, half_w, half_h, d[k]);
             }
-        }
-        if (j + step < n) {                                     // the next iteration's slot and indices
-            t_cur = slot_at(j + step, q_next);
-#pragma unroll
-            for (int k = 0; k < 3; k++) vi_cur[k] = vidx[3 * t_cur + k];
-        }
-        if (CL && j + 2u * step < n) q_next = cmap[b0 + j + 2u * step];
-        if (j < n) {
             if (fmaxf(fmaxf(d[0].rv.z, d[1].rv.z), d[2].rv.z) > kNear) {                  // :306
                 clip = fminf(fminf(d[0].rv.z, d[1].rv.z), d[2].rv.z) < kNear;             // :308, rare
                 if (!clip) live_t = raster_part(d, sw, sh, ts);

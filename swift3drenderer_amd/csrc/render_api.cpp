@@ -563,6 +563,7 @@ void dev_init(Dev &d, const HostScene &s) {
     // dispatched as soon as the previous frame's fragment workgroups free a slot
     int prio_least = 0, prio_greatest = 0;
     HIPCHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    // (the default priority instead measured the same for pipelined HBM frames, profiles/r05_order_ab.txt)
     for (hipStream_t &gs : d.geo) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
     HIPCHECK(hipMemcpy(d.vtx, s.vtx.data(), (size_t)g.nv * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d.nrm, s.nrm.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));

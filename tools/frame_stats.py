@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Diagnostic: walker iteration counters of the fragment kernel (librender_stats.so, -DS3R_STATS).
 
-    python tools/frame_stats.py [--scene full] [--pose P_over] [--width 3840] [--height 2160]
+    python tools/frame_stats.py [--scene full] [--pose P_over] [--width 3840] [--height 2160] [--device]
+
+--device: frames left in HBM (s3r_render_bands: k_geometry walks every segment start) instead of
+updateAndRender into a host buffer (row starts only, the fragment walks along its rows).
 """
 import argparse
 import ctypes
@@ -21,6 +24,7 @@ def main():
     ap.add_argument('--pose', default='P_over')
     ap.add_argument('--width', type=int, default=3840)
     ap.add_argument('--height', type=int, default=2160)
+    ap.add_argument('--device', action='store_true')
     a = ap.parse_args()
     from swift3drenderer_amd import build, poses, scene, renderer
     path = build.build_library(stats=True)
@@ -30,11 +34,19 @@ def main():
     data = os.path.join(d, a.scene + '.bin')
     scene.write_named(a.scene, data)
     r = renderer.Renderer(data)
+    if a.device:
+        import torch
+        buf = torch.empty((a.height, a.width), dtype=torch.int32, device='cuda')
+        st = torch.cuda.current_stream().cuda_stream
+        frame = lambda t: (r.render_bands(t, a.width, a.height, a.height, 1, 0, buf.data_ptr(), st),
+                           torch.cuda.synchronize())
+    else:
+        frame = lambda t: r.update_and_render(a.width, a.height, t)
     for t in poses.script(a.pose):
-        r.update_and_render(a.width, a.height, t)
+        frame(t)
     out = (ctypes.c_uint64 * 16)()
     lib.s3r_stats(out, 1)
-    r.update_and_render(a.width, a.height, poses.hold(a.pose))
+    frame(poses.hold(a.pose))
     lib.s3r_stats(out, 0)
     segs = (a.width + 1023) // 1024
     waves = a.height * segs

@@ -6,7 +6,7 @@ set -o pipefail
 for spec in "$@"; do
   IFS='|' read -r tag lib envs <<< "$spec"
   env $envs ${lib:+S3R_LIB=$lib} timeout -k 10 120 python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline $BENCH_EXTRA 2>/dev/null \
-    | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', round(d['value']), 'fps  frag_ms', d['fragment_kernel_ms'])" || exit 1
+    | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', round(d['value']), 'fps  device_fps', round(d['device_fps']), ' frag_ms', d['fragment_kernel_ms'])" || exit 1
 done
 # part 0 of 8 (one rank of an 8-GPU band split) when PARTS8=1
 if [ -n "$PARTS8" ]; then
