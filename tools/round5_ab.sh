@@ -1,0 +1,130 @@
+#!/bin/bash
+# Round 5's GPU-box experiments, one recipe each:  bash tools/round5_ab.sh <recipe>
+# Every recipe writes under gpurun_out/<recipe>/; the summaries kept are the profiles/r05_*.txt files
+# named beside each recipe.  Variant libraries (build/librender_<tag>.so) are made here beforehand with
+# swift3drenderer_amd.build.build_variant(tag, {defines}); ablation builds render wrong pixels on purpose.
+#
+#   check     the GPU suite with every launch checked (S3R_CHECK=1), then the in-process RCCL gather
+#             followed by the multi-device and tile suites         -> r05_gputest_check.log, r05_rccl_*.log
+#   measure   every part of the N-way splits (configs 3/4/5), 135-row stress bands, the 16-B record
+#             ablation (rec16), the 2-rank bench rehearsal, the unchecked suite after an RCCL gather
+#                                                                   -> r05_parts_all*.jsonl, r05_rec16_ablation.txt
+#   ntrec     raster records / bin entries stored non-temporal (ntrec / ntall builds) -> r05_ntrec_ab.txt
+#   tablewalk table walk vs the linear-run k_fragment (alltab / segst / at7a / at7b / tw8 / tw9 builds:
+#             parity of the row-path suites, frame rates, rocprof, SQ counters)
+#                                                                   -> r05_fragment_ab.txt, r05_alltab_pmc.txt,
+#                                                                      r05_fragment_occupancy_ab.txt, r05_tablewalk_tuning_ab.txt
+#   wgt       per-workgroup k_fragment timelines (wgt build): 4K whole frame (work-unit order and launch
+#             order) and part 0 of 8, raw dumps                     -> r05_order_ab.txt
+#   seg       k_fragment segment widths 6 / 3 / 2 / 1 chunks at 4K  (negative, DESIGN Row path)
+#   order     bin order by work units vs wall time (owall build): bench at 4K / 8K / P_id, part 0 of 8,
+#             pipelined periods, geometry priority, rocprof traces, diagnosis builds -> r05_order_ab.txt
+#   geo       k_geometry walk counters (stats build, --device) and per-workgroup timeline (wgt build)
+#   pf2       two-deep k_tile_setup pipeline vs the build before it  -> r05_setup_pf2_ab.txt
+#   defer     k_tile_setup binning pipelined one iteration deep (negative) -> r05_defer_bins_negative.txt
+#   tvruns    tile_visit key groups as runs of adjacent lanes vs the loop over distinct keys (tvloop
+#             build), and the branch-free raster pixel loop (tbl build), with SQ counters
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+R=${1:?recipe}
+OUT=gpurun_out/$R; mkdir -p "$OUT"
+D=/tmp/s3r_stress.bin
+stress_data() { [ -f $D ] || python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$D')"; }
+gpu_suite() {   # log, pytest args...
+  local log=$1; shift
+  timeout -k 10 900 python3 -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread "$@" > "$log" 2>&1 || { tail -30 "$log"; return 1; }
+  tail -1 "$log"
+}
+probe() {       # tag, env..., then overhead_probe args after --
+  local tag=$1; shift; local envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+  env "${envs[@]}" timeout -k 10 180 python3 tools/overhead_probe.py "$@" 2>/dev/null | grep '^{' | sed "s/^/$tag /" | cut -c1-200
+}
+
+case $R in
+check)
+  S3R_CHECK=1 gpu_suite $OUT/gputest_check.log tests || exit 1
+  S3R_CHECK=1 S3R_TEST_RCCL_INPROCESS=1 gpu_suite $OUT/rccl_experiment.log tests/test_multi.py::test_nccl_gather_in_process \
+      tests/test_multi_device.py tests/test_tiles.py || exit 1 ;;
+measure)
+  stress_data || exit 1
+  timeout -k 10 600 python3 -u tools/parts_all.py --configs 3,4,5 --out $OUT/parts_all.jsonl > $OUT/parts_all.log 2>&1 || exit 1
+  for n in 2 4; do timeout -k 10 300 python3 -u tools/parts_all.py --configs 5 --nparts $n --band 135 >> $OUT/parts_band135.jsonl || exit 1; done
+  PROF=1 PROF_NS="1" NS="1" bash tools/stress_lib_ab.sh "base||" "rec16|build/librender_rec16.so|" 2>&1 | tee $OUT/rec16_ab.txt || exit 1
+  timeout -k 10 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+      bench.py --gpus 2 --devices 0,0 --rank-devices 0,0 --gather-backend gloo --no-cpu-baseline > $OUT/bench_rehearsal2.log 2>&1 || exit 1
+  gpu_suite $OUT/bench_ranks_gpu.log tests/test_bench_ranks.py || exit 1
+  S3R_TEST_RCCL_INPROCESS=1 gpu_suite $OUT/rccl_unchecked.log -s tests/test_multi.py::test_nccl_gather_in_process tests || exit 1 ;;
+ntrec)
+  stress_data || exit 1
+  NS="1 8" BAND=135 PROF=1 PROF_NS="1" bash tools/stress_lib_ab.sh "base||" "ntrec|build/librender_ntrec.so|" \
+      "ntall|build/librender_ntall.so|" "base2||" 2>&1 | tee $OUT/ntrec_ab.txt ;;
+tablewalk)
+  for v in alltab segst at7a at7b tw8 tw9; do
+    S3R_LIB=build/librender_$v.so gpu_suite $OUT/${v}_parity.log tests/test_gpu_parity.py tests/test_multi_device.py tests/test_multi.py || exit 1
+  done
+  PARTS8=1 bash tools/lib_ab.sh "base||" "alltab|build/librender_alltab.so|" "segst|build/librender_segst.so|" \
+      "at7a|build/librender_at7a.so|" "at7b|build/librender_at7b.so|" "tw8|build/librender_tw8.so|" \
+      "base_wf||S3R_WATERFALL_BINS=0" "base2||" 2>&1 | tee $OUT/ab.txt || exit 1
+  cp swift3drenderer_amd/librender.so build/librender_prod.so
+  S3R_VARIANTS='{"prod": {}, "alltab": {}, "segst": {}, "at7a": {}, "tw8": {}, "tw9": {}}' S3R_VARIANT_BENCH="--scene full --pose P_over" \
+      timeout -k 10 900 python3 tools/variants.py run 2>&1 | tee -a $OUT/ab.txt || exit 1
+  find gpurun_out/variants \( -name '*kernel_trace.csv' -o -name '*agent_info.csv' \) -delete
+  bash tools/variant_pmc.sh $OUT/vpmc prod alltab segst 2>&1 | tee $OUT/pmc.txt ;;
+wgt)
+  S3R_WGT_DUMP=$OUT/n1.npy timeout -k 10 240 python3 -u tools/wg_timeline.py > $OUT/n1.txt 2>&1 &&
+  S3R_LPT_MIN=100000000 S3R_WGT_DUMP=$OUT/n1_nolpt.npy timeout -k 10 240 python3 -u tools/wg_timeline.py > $OUT/n1_nolpt.txt 2>&1 &&
+  S3R_WGT_DUMP=$OUT/n8.npy timeout -k 10 240 python3 -u tools/wg_timeline.py --nparts 8 > $OUT/n8.txt 2>&1 ;;
+seg)
+  PARTS8=1 bash tools/lib_ab.sh 'base||' 'seg3||S3R_SEG3=1 S3R_MIN_BLOCKS=6000' 'seg2||S3R_MIN_BLOCKS=8000' \
+      'seg1||S3R_MIN_BLOCKS=20000' 'base2||' 2>&1 | tee $OUT/ab.txt ;;
+order)
+  W=build/librender_owall.so
+  PARTS8=1 bash tools/lib_ab.sh 'work||' "wall|$W|" 'work2||' "wall2|$W|" 2>&1 | tee $OUT/ab4k.txt || exit 1
+  BENCH_EXTRA='--width 7680 --height 4320' bash tools/lib_ab.sh 'work 8K||' "wall 8K|$W|" 2>&1 | tee $OUT/ab8k.txt || exit 1
+  BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'work P_id||' "wall P_id|$W|" 2>&1 | tee $OUT/abpid.txt || exit 1
+  for rep in 1 2; do
+    for spec in "work|" "wall|S3R_LIB=$W" "wsky|S3R_LIB=build/librender_wsky.so" "wgeo|S3R_LIB=build/librender_wgeo.so" \
+                "owgeo|S3R_LIB=build/librender_owgeo.so"; do
+      IFS='|' read -r tag envs <<< "$spec"
+      probe $tag $envs -- --steps 2000 | tee -a $OUT/probe.txt || exit 1
+    done
+  done
+  for spec in "work|" "wall|$W"; do
+    IFS='|' read -r tag lib <<< "$spec"
+    S3R_LIB=$lib timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/tr_$tag -o tr -- \
+        python3 tools/overhead_probe.py --steps 300 > $OUT/tr_$tag.log 2>&1 || exit 1
+    f=$(find $OUT/tr_$tag -name '*kernel_trace.csv' | head -1)
+    python3 tools/trace_timeline.py "$f" --first 200 --count 12 > $OUT/timeline_$tag.txt || exit 1
+    rm -f "$f"
+  done ;;
+geo)
+  timeout -k 10 180 python3 tools/frame_stats.py --device > $OUT/stats_dev.txt 2>&1 || exit 1
+  S3R_SERIAL=1 timeout -k 10 180 python3 tools/geo_timeline.py > $OUT/serial.txt 2>&1 || exit 1
+  timeout -k 10 180 python3 tools/geo_timeline.py > $OUT/pipelined.txt 2>&1 ;;
+pf2)
+  gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'pf2||' 'old|build/librender_old.so|' 'pf2b||' \
+      'oldb|build/librender_old.so|' 2>&1 | tee $OUT/stress_ab.txt ;;
+defer)
+  gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1" bash tools/stress_lib_ab.sh 'defer|build/librender_defer.so|' 'base||' \
+      'defer_g256|build/librender_defer.so|S3R_TILE_GRID=256' 'base_g256||S3R_TILE_GRID=256' \
+      'defer_g64|build/librender_defer.so|S3R_TILE_GRID=64' 'base_g64||S3R_TILE_GRID=64' 2>&1 | tee $OUT/ab.txt ;;
+tvruns)
+  S3R_LIB=build/librender_tbl.so gpu_suite $OUT/tests.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'runs||' 'loop|build/librender_tvloop.so|' 'tbl|build/librender_tbl.so|' \
+      'runs2||' 'loop2|build/librender_tvloop.so|' 'tbl2|build/librender_tbl.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  for spec in 'runs|' 'loop|build/librender_tvloop.so' 'tbl|build/librender_tbl.so'; do
+    IFS='|' read -r tag lib <<< "$spec"
+    S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+        SQ_BUSY_CYCLES --output-format csv -d "$PWD/$OUT/pmc_$tag" -o run -- python3 tools/overhead_probe.py --scene icosa-stress \
+        --pose P_id --data $D --steps 10 > $OUT/pmc_$tag.log 2>&1 || { tail -5 $OUT/pmc_$tag.log; exit 1; }
+    python3 tools/pmc_summary.py $OUT/pmc_$tag --last 10 > $OUT/pmc_$tag.txt 2>&1 || true
+    find $OUT/pmc_$tag -name '*.csv' -size +5M -delete
+  done ;;
+*)
+  echo "unknown recipe $R"; exit 2 ;;
+esac
