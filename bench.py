@@ -555,6 +555,13 @@ def run_rank0(a, N, np, torch):
     frag_avg_s = frag_ms / 1e3 / max(nfr, 1)
     achieved = frag_bytes / frag_avg_s / 1e9
     workload = f'{a.scene}/{a.pose}/{W}x{H}/N1'
+    if path == 2 and device_fps:
+        # the tile path reads no per-vertex attributes beyond the winners' (§8(d)'s 48 A bytes are not its
+        # traffic): the PMC-measured bytes of its setup and fused raster per frame over the device frame
+        cb = [load_traffic(workload, 'setup_hbm_bytes_per_launch'), load_traffic(workload)]
+        if all(cb):
+            frame_roof['counter_bytes_per_frame'] = int(sum(cb))
+            frame_roof['counter_frac_device'] = round(sum(cb) * device_fps / 1e9 / HBM_PEAK_GBS, 5)
 
     cpu = None
     if not a.no_cpu_baseline and len(devices) == 1:

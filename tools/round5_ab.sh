@@ -23,7 +23,11 @@
 #   pf2       two-deep k_tile_setup pipeline vs the build before it  -> r05_setup_pf2_ab.txt
 #   defer     k_tile_setup binning pipelined one iteration deep (negative) -> r05_defer_bins_negative.txt
 #   tvruns    tile_visit key groups as runs of adjacent lanes vs the loop over distinct keys (tvloop
-#             build), and the branch-free raster pixel loop (tbl build), with SQ counters
+#             build), and the branch-free raster pixel loop (tbl build), with SQ counters; the stress
+#             frame's staged / depth-culled (slot, tile) pairs (stats build); tab8: the raster's row and x
+#             walks replaced by one multiply-add (timing only); trs: each staged triangle's walk down to
+#             the tile's first row done once at staging (S3R_TROWSTART)
+#   ob        the longest-first order's cost buckets at 1/8 octave (ob8 build) instead of 1/4
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=${1:?recipe}
@@ -114,9 +118,12 @@ defer)
       'defer_g64|build/librender_defer.so|S3R_TILE_GRID=64' 'base_g64||S3R_TILE_GRID=64' 2>&1 | tee $OUT/ab.txt ;;
 tvruns)
   S3R_LIB=build/librender_tbl.so gpu_suite $OUT/tests.log tests/test_tiles.py || exit 1
+  S3R_LIB=build/librender_trs.so gpu_suite $OUT/tests_trs.log tests/test_tiles.py || exit 1
+  timeout -k 10 300 python3 tools/tile_stats.py > $OUT/tile_stats.txt 2>&1 || { tail -5 $OUT/tile_stats.txt; exit 1; }
+  cat $OUT/tile_stats.txt
   stress_data || exit 1
   NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'runs||' 'loop|build/librender_tvloop.so|' 'tbl|build/librender_tbl.so|' \
-      'runs2||' 'loop2|build/librender_tvloop.so|' 'tbl2|build/librender_tbl.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+      'runs2||' 'loop2|build/librender_tvloop.so|' 'tbl2|build/librender_tbl.so|' 'tab8|build/librender_tab8.so|' 'trs|build/librender_trs.so|' 'trs2|build/librender_trs.so|' 2>&1 | tee $OUT/ab.txt || exit 1
   for spec in 'runs|' 'loop|build/librender_tvloop.so' 'tbl|build/librender_tbl.so'; do
     IFS='|' read -r tag lib <<< "$spec"
     S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
@@ -125,6 +132,9 @@ tvruns)
     python3 tools/pmc_summary.py $OUT/pmc_$tag --last 10 > $OUT/pmc_$tag.txt 2>&1 || true
     find $OUT/pmc_$tag -name '*.csv' -size +5M -delete
   done ;;
+ob)
+  PARTS8=1 bash tools/lib_ab.sh 'base||' 'ob8|build/librender_ob8.so|' 'base2||' 'ob8b|build/librender_ob8.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'base P_id||' 'ob8 P_id|build/librender_ob8.so|' 2>&1 | tee -a $OUT/ab.txt ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
