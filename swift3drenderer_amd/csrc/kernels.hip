@@ -485,10 +485,14 @@ uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
 // values from another frame size are only hints; no fragment launch of the set runs meanwhile, so
 // both passes read the same values) into kOrderBuckets quarter-octave buckets,
 // costliest first; perm is always a permutation of [0, n).
-constexpr uint32_t kOrderBuckets = 32;
-// bucket of a cost: a quarter octave each from 2^6 units (a sky bin: kWorkSky) -- no max pass over the costs
+#ifndef S3R_ORDER_STEPS
+#define S3R_ORDER_STEPS 4              // buckets per octave of cost
+#endif
+constexpr uint32_t kOrderSteps = S3R_ORDER_STEPS, kOrderBuckets = 8u * kOrderSteps;
+// bucket of a cost: 1 / kOrderSteps octave each over 8 octaves from 2^6 units (a sky bin: kWorkSky) --
+// no max pass over the costs
 __device__ __forceinline__ uint32_t order_bucket(uint32_t c) {
-    const float l = __log2f((float)max(c, 64u)) * 4.0f - 24.0f;
+    const float l = __log2f((float)max(c, 64u)) * (float)kOrderSteps - 6.0f * (float)kOrderSteps;
     return min((uint32_t)l, kOrderBuckets - 1u);
 }
 // the two passes read kOrderUnroll costs per thread before using them (independent loads in flight)
@@ -1543,15 +1547,24 @@ __device__ __forceinline__ void tile_visit(const TileSpan &sp, uint32_t tiles_x,
             if (sp.n >= (1u << 18)) ky = k / sp.ntx;          // (beyond udiv_small's range: huge boxes)
             key[q] = act ? ((sp.ty0 + ky) * tiles_x + sp.tx0 + k - ky * sp.ntx) * kDepthBuckets + sp.bucket
                          : 0xFFFFFFFFu;
-            uint64_t todo = __ballot(act);
             uint32_t my_leader = 0, my_rank = 0, cnt = 0;
-            while (todo) {
-                const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
-                const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key[q], (int)leader);
-                const uint64_t grp = __ballot(act && key[q] == lk);
-                if (act && key[q] == lk) { my_leader = leader; my_rank = lane_prefix(grp, lane); }
-                if (lane == leader) cnt = (uint32_t)__builtin_popcountll(grp);
-                todo &= ~grp;
+            // groups = runs of adjacent lanes with one key (consecutive triangles of a mesh share
+            // tiles): a constant number of instructions per step, where a loop over the distinct keys
+            // took one ballot round each; equal keys in separate runs take separate atomics (stress
+            // setup: 259 -> 218 M VALU, 79 -> 59 M SALU wave-instructions, time equal, part 0 of 8
+            // +2 %; profiles/r05_tvruns_ab.txt)
+            const uint32_t prevk = (uint32_t)__shfl_up((int)key[q], 1);
+            const bool head = act && (lane == 0u || prevk != key[q]);
+            const uint64_t heads = __ballot(head);
+            const uint64_t stops = heads | ~__ballot(act);             // a run ends at a head or an idle lane
+            const uint64_t upto = (2ull << lane) - 1ull;                // lanes <= this one (lane 63: all)
+            if (act) {
+                my_leader = 63u - (uint32_t)__builtin_clzll(heads & upto);
+                my_rank = lane - my_leader;
+            }
+            if (head) {
+                const uint64_t after = stops & ~upto;
+                cnt = (after ? (uint32_t)__builtin_ctzll(after) : 64u) - lane;
             }
             leader_of[q] = my_leader;
             rank[q] = my_rank;

@@ -28,6 +28,8 @@ def main():
     ap.add_argument('--height', type=int, default=2160)
     ap.add_argument('--nparts', type=int, default=1)
     ap.add_argument('--band', type=int, default=16)
+    ap.add_argument('--delivered', action='store_true',
+                    help='updateAndRender frames into a host buffer (row starts only) instead of HBM frames')
     a = ap.parse_args()
     import torch
     from swift3drenderer_amd import poses, renderer, scene
@@ -42,14 +44,21 @@ def main():
     r = renderer.Renderer(data, device=0)
     buf = torch.empty((H, W), dtype=torch.int32, device='cuda')
     st = torch.cuda.current_stream().cuda_stream
+    host = np.empty((H, W), dtype=np.uint32)
+
+    def frame(t):
+        if a.delivered:
+            r.update_and_render(W, H, t, host)
+        else:
+            r.render_bands(t, W, H, B, N, 0, buf.data_ptr(), st)
     for t in poses.script(a.pose):
-        r.render_bands(t, W, H, B, N, 0, buf.data_ptr(), st)
+        frame(t)
     for _ in range(20):
-        r.render_bands(poses.hold(a.pose), W, H, B, N, 0, buf.data_ptr(), st)
+        frame(poses.hold(a.pose))
     torch.cuda.synchronize()
     out = (ctypes.c_uint64 * (4 * 16384))()
     lib.s3r_stats_geo_times(out, 16384)           # clear
-    r.render_bands(poses.hold(a.pose), W, H, B, N, 0, buf.data_ptr(), st)
+    frame(poses.hold(a.pose))
     torch.cuda.synchronize()
     n = lib.s3r_stats_geo_times(out, 16384)
     t = np.frombuffer(out, dtype=np.uint64)[: 4 * n].reshape(n, 4).astype(np.int64)

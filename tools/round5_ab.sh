@@ -19,7 +19,8 @@
 #   seg       k_fragment segment widths 6 / 3 / 2 / 1 chunks at 4K  (negative, DESIGN Row path)
 #   order     bin order by work units vs wall time (owall build): bench at 4K / 8K / P_id, part 0 of 8,
 #             pipelined periods, geometry priority, rocprof traces, diagnosis builds -> r05_order_ab.txt
-#   geo       k_geometry walk counters (stats build, --device) and per-workgroup timeline (wgt build)
+#   geo       k_geometry walk counters (stats build, --device) and per-workgroup timelines (wgt build:
+#             HBM frames serialised / pipelined, delivered frames), a kernel trace of delivered frames
 #   pf2       two-deep k_tile_setup pipeline vs the build before it  -> r05_setup_pf2_ab.txt
 #   defer     k_tile_setup binning pipelined one iteration deep (negative) -> r05_defer_bins_negative.txt
 #   tvruns    tile_visit key groups as runs of adjacent lanes vs the loop over distinct keys (tvloop
@@ -104,7 +105,13 @@ order)
 geo)
   timeout -k 10 180 python3 tools/frame_stats.py --device > $OUT/stats_dev.txt 2>&1 || exit 1
   S3R_SERIAL=1 timeout -k 10 180 python3 tools/geo_timeline.py > $OUT/serial.txt 2>&1 || exit 1
-  timeout -k 10 180 python3 tools/geo_timeline.py > $OUT/pipelined.txt 2>&1 ;;
+  timeout -k 10 180 python3 tools/geo_timeline.py > $OUT/pipelined.txt 2>&1 || exit 1
+  timeout -k 10 180 python3 tools/geo_timeline.py --delivered > $OUT/delivered.txt 2>&1 || exit 1
+  S3R_LIB= timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/tr -o tr -- \
+      python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-device > $OUT/tr.log 2>&1 || exit 1
+  f=$(find $OUT/tr -name '*kernel_trace.csv' | head -1)
+  python3 tools/trace_timeline.py "$f" --first -40 --count 8 > $OUT/timeline_delivered.txt || exit 1
+  rm -f "$f" ;;
 pf2)
   gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
   stress_data || exit 1
@@ -126,7 +133,7 @@ tvruns)
       'runs2||' 'loop2|build/librender_tvloop.so|' 'tbl2|build/librender_tbl.so|' 'tab8|build/librender_tab8.so|' 'trs|build/librender_trs.so|' 'trs2|build/librender_trs.so|' 2>&1 | tee $OUT/ab.txt || exit 1
   for spec in 'runs|' 'loop|build/librender_tvloop.so' 'tbl|build/librender_tbl.so'; do
     IFS='|' read -r tag lib <<< "$spec"
-    S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+    env S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
         SQ_BUSY_CYCLES --output-format csv -d "$PWD/$OUT/pmc_$tag" -o run -- python3 tools/overhead_probe.py --scene icosa-stress \
         --pose P_id --data $D --steps 10 > $OUT/pmc_$tag.log 2>&1 || { tail -5 $OUT/pmc_$tag.log; exit 1; }
     python3 tools/pmc_summary.py $OUT/pmc_$tag --last 10 > $OUT/pmc_$tag.txt 2>&1 || true

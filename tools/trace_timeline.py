@@ -23,7 +23,7 @@ def main():
             rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), name))
     rows.sort()
     frags = [r for r in rows if a.frag in r[2]]
-    win = frags[a.first:a.first + a.count]
+    win = frags[a.first:][:a.count]                 # (a negative --first counts from the last launch)
     if not win:
         raise SystemExit('no fragment launches in the window')
     t0, t1 = win[0][0], win[-1][1]
