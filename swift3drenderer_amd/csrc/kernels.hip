@@ -486,7 +486,7 @@ uint32_t start_entries(uint32_t W) { return start_entries_of(W); }
 // both passes read the same values) into kOrderBuckets quarter-octave buckets,
 // costliest first; perm is always a permutation of [0, n).
 #ifndef S3R_ORDER_STEPS
-#define S3R_ORDER_STEPS 4              // buckets per octave of cost
+#define S3R_ORDER_STEPS 8              // buckets per octave of cost (4: 50.9 vs 50.5 us at 4K, profiles/r05_order_ab.txt)
 #endif
 constexpr uint32_t kOrderSteps = S3R_ORDER_STEPS, kOrderBuckets = 8u * kOrderSteps;
 // bucket of a cost: 1 / kOrderSteps octave each over 8 octaves from 2^6 units (a sky bin: kWorkSky) --
@@ -623,7 +623,8 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     uint32_t ntri, Mat34 m, float factor, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part,
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
     float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
-    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky, uint32_t row_starts) {
+    uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky, uint32_t row_starts,
+    uint32_t nslots) {
     __shared__ TriSetup sts;
     extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
     // slot-major 1-D grid: workgroup 0 (with `order`) computes this frame's fragment order, then the
@@ -638,7 +639,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     }
     const uint32_t pub0 = order ? 1u : 0u, first = pub0 + (sky.flags ? nrb : 0u);   // publishers, geometry
     if (sky.flags && g0 < first) {
-        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, 2u * ntri);
+        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, nslots);
         return;
     }
     const uint32_t tid = threadIdx.x, gs = g0 - first, slot = gs / nrb, rb = gs - slot * nrb;
@@ -652,6 +653,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
         geo_slot_setup(slot, ntri, vtx, nrm, pay, disc, vidx, aidx, m, factor, (float)W, (float)H, t);
         sts = t;
         if (rb == 0) tris[slot] = t;
+        if (rb == 0 && nslots == ntri) tris[ntri + slot].kind = kDead;   // (clip slots left out: dead)
 #ifdef S3R_STATS
         atomicMax(&g_tstats[0], wall_clock64() - t_start);
 #endif
@@ -2662,17 +2664,18 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order, const GeoSkyFlags *gsf, bool row_starts) {
+                     uint32_t *order, const GeoSkyFlags *gsf, bool row_starts, bool clip_slots) {
+    const uint32_t nslots = clip_slots ? 2u * ntri : ntri;
     const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
     if (ntri == 0 || rows_local == 0 || (gsf && nrb > kGeoCntMax)) {
         // nothing to set up (every bin is sky), or more row blocks than counters: k_sky_flags publishes
         if (ntri && rows_local) {
             const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-            { hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
+            { hipExtLaunchKernelGGL(k_geometry, dim3(nslots * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
                                   st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
                                   nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
                                   (uint32_t)fragment_bins(W, rows_local), order, nrb,
-                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u); after_launch("k_geometry", st); }
+                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u, nslots); after_launch("k_geometry", st); }
         }
         if (gsf)
             launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
@@ -2686,10 +2689,10 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    { hipExtLaunchKernelGGL(k_geometry, dim3(2 * ntri * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
+    { hipExtLaunchKernelGGL(k_geometry, dim3(nslots * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u); after_launch("k_geometry", st); }
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u, nslots); after_launch("k_geometry", st); }
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

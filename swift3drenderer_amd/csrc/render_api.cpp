@@ -77,6 +77,7 @@ constexpr uint64_t kLptMinBins = 2000;      // longest-first fragment order from
 // Slots above which the row path's start table (2T x H x segments x 16 B) is not worth building:
 // the order-independent tile path takes over (the icosahedron stress scene).
 constexpr uint64_t kRowPathMaxSlots = 8192;
+constexpr uint64_t kNearCheckMaxTri = 1024;   // the host's near-plane check: scenes up to this many triangles
 constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
 constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set
 constexpr int kMaxDevices = 64;
@@ -330,6 +331,12 @@ struct Lib {
     uint32_t nv = 0, na = 0, ntri = 0, ntex = 0;
     uint64_t nindices = 0;
     uint32_t ncl = 0;                          // clusters (clusters.cpp; 0: the scene has none)
+    // row-path scenes up to kNearCheckMaxTri triangles: positions and vertex indices kept on the host
+    // for the per-frame near-plane check (near_plane_crossing)
+    std::vector<float4> near_vtx;
+    std::vector<uint32_t> near_vidx;
+    std::vector<uint8_t> near_side;
+    bool clip_slots = true;                    // this frame: launch k_geometry's clip-appended slots
     bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
     bool clusters_whole = false;               // ... also for whole frames (S3R_CLUSTERS=2)
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
@@ -526,6 +533,8 @@ HostScene read_scene() {
     }
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
+    g.near_vtx.clear(); g.near_vidx.clear();
+    if (ntri <= kNearCheckMaxTri && 2 * ntri <= kRowPathMaxSlots) { g.near_vtx = s.vtx; g.near_vidx = s.vidx; }
     // clusters for the tile path's per-frame cull (scenes the tile path renders by default, or any
     // scene with S3R_CLUSTERS=2): connected meshes of 8-32 triangles, larger ones cut, smaller pooled
     const char *ce = getenv("S3R_CLUSTERS");
@@ -730,6 +739,8 @@ void release_all() {
     g.band_rows = band;
 }
 
+bool near_plane_crossing();
+
 // render.cpp:266-280: first-call init, camera, resize.
 void frame_begin(const Input *input, uint32_t width, uint32_t height) {
     if (!g.initialized) {
@@ -746,6 +757,7 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
         g.factor = kNear * (float)height / (2 * config_scale());          // render.cpp:279
         unregister_all();
     }
+    g.clip_slots = near_plane_crossing();
 }
 
 TimingSlot *timing_slot(Dev &d) {
@@ -829,6 +841,34 @@ void wait_all_fragments(Dev &d, hipStream_t geo) {
     for (int q = 0; q < kSets; q++) HIPCHECK(hipStreamWaitEvent(geo, d.frag_done[q], 0));
 }
 
+
+// Can any triangle cross the near plane this frame (render.cpp:308: some corner in front of it, some
+// behind)?  If not, k_geometry leaves out the clip-appended slots (launch_geometry clip_slots).  Each
+// vertex's camera depth nz = -(row 2 of the camera matrix . v) (render.cpp:286) is classified against
+// kNear with a margin far above float rounding (1e-4 of the summed term magnitudes): a vertex inside
+// the margin, or a non-finite one, counts as crossing.  Scenes without the host copy: always true.
+#ifndef S3R_NEAR_CHECK
+#define S3R_NEAR_CHECK 1
+#endif
+bool near_plane_crossing() {
+    if (!S3R_NEAR_CHECK || g.near_vidx.empty()) return true;
+    const size_t nv = g.near_vtx.size();
+    g.near_side.resize(nv);
+    const float *r = g.m.m[2];
+    for (size_t i = 0; i < nv; i++) {
+        const float4 v = g.near_vtx[i];
+        const float a = r[0] * v.x, b = r[1] * v.y, c = r[2] * v.z, e = r[3] * v.w;
+        const float nz = -(((a + b) + c) + e);
+        const float margin = 1e-4f * (fabsf(a) + fabsf(b) + fabsf(c) + fabsf(e)) + 1e-6f;
+        if (!std::isfinite(nz) || !std::isfinite(margin) || fabsf(nz - kNear) <= margin) return true;
+        g.near_side[i] = nz > kNear ? 1u : 2u;          // 1: in front of the near plane, 2: behind it
+    }
+    for (size_t t = 0; t + 2 < g.near_vidx.size(); t += 3) {
+        const uint8_t m = g.near_side[g.near_vidx[t]] | g.near_side[g.near_vidx[t + 1]] | g.near_side[g.near_vidx[t + 2]];
+        if (m == 3u) return true;
+    }
+    return false;
+}
 
 bool use_tile_path() {
     if (g.raster_path == 1) return false;
@@ -1294,7 +1334,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     }
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
-                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts);
+                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts, g.clip_slots);
     d.hp.lap(3);
     if (ts) HIPCHECK(hipEventRecord(ts->geo1, geo));
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first

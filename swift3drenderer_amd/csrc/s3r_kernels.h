@@ -60,11 +60,15 @@ struct GeoSkyFlags {
     uint32_t *flags, *probe, *geo_cnt;
     uint32_t tag, gpu_eighths;
 };
+// clip_slots = false: no triangle can cross the near plane this frame (the host's check,
+// render_api.cpp near_plane_crossing), so the launch leaves out the clip-appended slots T..2T-1 (their
+// records are marked dead) -- half the workgroups, one dispatch round fewer for small scenes.
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order, const GeoSkyFlags *gsf = nullptr, bool row_starts = false);
+                     uint32_t *order, const GeoSkyFlags *gsf = nullptr, bool row_starts = false,
+                     bool clip_slots = true);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();

@@ -29,6 +29,8 @@
 #             walks replaced by one multiply-add (timing only); trs: each staged triangle's walk down to
 #             the tile's first row done once at staging (S3R_TROWSTART)
 #   ob        the longest-first order's cost buckets at 1/8 octave (ob8 build) instead of 1/4
+#   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
+#             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=${1:?recipe}
@@ -142,6 +144,14 @@ tvruns)
 ob)
   PARTS8=1 bash tools/lib_ab.sh 'base||' 'ob8|build/librender_ob8.so|' 'base2||' 'ob8b|build/librender_ob8.so|' 2>&1 | tee $OUT/ab.txt || exit 1
   BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'base P_id||' 'ob8 P_id|build/librender_ob8.so|' 2>&1 | tee -a $OUT/ab.txt ;;
+nearck)
+  gpu_suite $OUT/parity.log tests/test_gpu_parity.py tests/test_host_loop.py tests/test_multi_device.py tests/test_abi.py || exit 1
+  timeout -k 10 180 python3 tools/geo_timeline.py --delivered > $OUT/geo_delivered.txt 2>&1 || exit 1
+  for rep in 1 2; do
+    bash tools/lib_ab.sh 'check||' 'nocheck|build/librender_noclipck.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'check P_id||' 'nocheck P_id|build/librender_noclipck.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'check 1080p||' 'nocheck 1080p|build/librender_noclipck.so|' 2>&1 | tee -a $OUT/ab.txt ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
