@@ -55,6 +55,18 @@ def test_frame_matches_oracle(gpu_renderer, scene_dir, scene_name, pose, w, h):
     assert np.array_equal(got, want), diff_report(got, want)
 
 
+def test_clip_slots_follow_the_near_plane(gpu_renderer, scene_dir):
+    """k_geometry leaves out the clip-appended slots (and marks their records dead) when the host finds
+    no triangle crossing the near plane (render_api.cpp near_plane_crossing, render.cpp:308): poses that
+    cross it and poses that do not, alternating in one session, each frame against the oracle."""
+    path = scene_dir['full']
+    for pose in ['P_clip', 'P_over', 'P_clip', 'P_id', 'P_clip', 'P_floor']:
+        script = poses.script(pose)
+        want = oracle_render_pose(path, script, 640, 480, extra_frames=1)
+        got = render_pose(gpu_renderer, path, script, 640, 480, extra_frames=1)
+        assert np.array_equal(got, want), (pose, diff_report(got, want))
+
+
 def test_resize_between_calls(gpu_renderer, scene_dir):
     """render.cpp:275-280: factor changes only when W*H changes; camera state carries over."""
     from oracle.oracle import OracleRenderer
