@@ -1290,7 +1290,12 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     const char *lpt_env = getenv("S3R_LPT_MIN");            // tuning / test override
     // (delivered frames are bound by the link, not by their heaviest bins: launch order, no order
     // column; measured equal or 1 us better)
-    const bool lpt = g.ntri > 0 && !hf && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins);
+    // ... and only for the widest (6-chunk) bins: with 2-chunk bins (1080p, 4K parts of 4 and 8) the launch
+    // order measured best (1080p flat, k_fragment: launch order 24.2-24.3 us, wall-time order 25.0-25.3,
+    // work-unit order 27.5-28.1; profiles/r05_order_ab.txt) -- short bins leave no long tail to fix,
+    // and heavy-first groups the textured floor's bins on the chip at once
+    const bool lpt = g.ntri > 0 && !hf && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins) &&
+                     (lpt_env || fragment_segment_pixels() >= 384u);     // (6 chunks of 64 px)
     if (lpt && d.order_cap < bins) {
         HIPCHECK(hipDeviceSynchronize());
         for (int q = 0; q < kSets; q++) {

@@ -29,6 +29,7 @@
 #             walks replaced by one multiply-add (timing only); trs: each staged triangle's walk down to
 #             the tile's first row done once at staging (S3R_TROWSTART)
 #   ob        the longest-first order's cost buckets at 1/8 octave (ob8 build) instead of 1/4
+#   order1080 the bin orders (work units / wall time / launch order) at 1080p (flat, full) and 4K
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -152,6 +153,14 @@ nearck)
   done
   BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'check P_id||' 'nocheck P_id|build/librender_noclipck.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
   BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'check 1080p||' 'nocheck 1080p|build/librender_noclipck.so|' 2>&1 | tee -a $OUT/ab.txt ;;
+order1080)
+  for rep in 1 2; do
+    BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'work 1080p||' 'wall 1080p|build/librender_owall.so|' \
+        'launch 1080p||S3R_LPT_MIN=100000000' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  BENCH_EXTRA='--scene full --width 1920 --height 1080' bash tools/lib_ab.sh 'work full1080||' 'wall full1080|build/librender_owall.so|' \
+      'launch full1080||S3R_LPT_MIN=100000000' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  bash tools/lib_ab.sh 'work 4K||' 'wall 4K|build/librender_owall.so|' 'launch 4K||S3R_LPT_MIN=100000000' 2>&1 | tee -a $OUT/ab.txt ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
