@@ -2134,7 +2134,13 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
 // the split form -- keys through HBM, a per-pixel resolve launch -- slower everywhere: stress scene
 // whole frame 800 -> 854 fps fused, delivered 583 -> 614, part 0 of 8 4 491 -> 4 672; it is gone.)
 template <uint32_t STAGE = kTileStage>
-__global__ void __launch_bounds__(kTileThreads) k_tile_raster(
+#ifndef S3R_TOCC
+#define S3R_TOCC 6                     // min waves per SIMD of the fused raster: 80 VGPRs (92 uncapped, occupancy 5);
+#endif                                 // the 256-stage instance stays at 4 (its LDS).  Stress scene, one box
+                                       // (profiles/r05_raster_occ_ab.txt): raster 462 -> 430 us serialised, whole
+                                       // frame pipelined 1 030-1 036 -> 1 068-1 083 fps; 7 (72 VGPRs, 12 spilled):
+                                       // the same raster time, part 0 of 8 -2.5 %
+__global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
     const uint32_t *__restrict__ list, uint32_t cap,

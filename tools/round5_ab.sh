@@ -30,6 +30,11 @@
 #             the tile's first row done once at staging (S3R_TROWSTART)
 #   ob        the longest-first order's cost buckets at 1/8 octave (ob8 build) instead of 1/4
 #   order1080 the bin orders (work units / wall time / launch order) at 1080p (flat, full) and 4K
+#   georows   k_geometry row blocks of 256 / 320 rows (geo256 / geo320 builds) instead of 128
+#   rasterpf  fused raster: list entries prefetched two stages ahead (tpf2), one 16-B read per row in the
+#             per-triangle depth cull (tzv4), occupancy caps 5 / 6 (o5 / o6 builds, S3R_TOCC)
+#   rasterocc fused raster occupancy caps 6 / 7 (to6 / to7), and 128-triangle stages for delivered frames
+#             at occupancy 6 (to6l128): stress N=1 / part 0 of 8, delivered and device bench lines
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -161,6 +166,29 @@ order1080)
   BENCH_EXTRA='--scene full --width 1920 --height 1080' bash tools/lib_ab.sh 'work full1080||' 'wall full1080|build/librender_owall.so|' \
       'launch full1080||S3R_LPT_MIN=100000000' 2>&1 | tee -a $OUT/ab.txt || exit 1
   bash tools/lib_ab.sh 'work 4K||' 'wall 4K|build/librender_owall.so|' 'launch 4K||S3R_LPT_MIN=100000000' 2>&1 | tee -a $OUT/ab.txt ;;
+georows)
+  S3R_LIB=build/librender_geo256.so gpu_suite $OUT/parity256.log tests/test_gpu_parity.py tests/test_multi_device.py tests/test_host_loop.py || exit 1
+  for rep in 1 2; do
+    bash tools/lib_ab.sh 'g128||' 'g256|build/librender_geo256.so|' 'g320|build/librender_geo320.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  PARTS8=1 bash tools/lib_ab.sh 'g128 P_id||' 'g256 P_id|build/librender_geo256.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'g128 1080p||' 'g256 1080p|build/librender_geo256.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--width 7680 --height 4320' bash tools/lib_ab.sh 'g128 8K||' 'g256 8K|build/librender_geo256.so|' 2>&1 | tee -a $OUT/ab.txt ;;
+rasterpf)
+  S3R_LIB=build/librender_tbotho5.so gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1" bash tools/stress_lib_ab.sh 'base||' 'tpf2|build/librender_tpf2.so|' 'tzv4|build/librender_tzv4.so|' \
+      'tpf2o5|build/librender_tpf2o5.so|' 'tbotho5|build/librender_tbotho5.so|' 'to6|build/librender_to6.so|' \
+      'tbotho6|build/librender_tbotho6.so|' 'base2||' 2>&1 | tee $OUT/ab.txt ;;
+rasterocc)
+  S3R_LIB=build/librender_to6l128.so gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1" bash tools/stress_lib_ab.sh 'base||' 'to6|build/librender_to6.so|' 'to7|build/librender_to7.so|' \
+      'base2||' 'to6b|build/librender_to6.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  for rep in 1 2; do
+    BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'base stress||' 'to6 stress|build/librender_to6.so|' \
+        'to6l128 stress|build/librender_to6l128.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
