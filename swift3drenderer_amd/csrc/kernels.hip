@@ -1816,6 +1816,8 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_
 // wholly past the near plane is set up here (emit_slot); one that crosses it (render.cpp:308, rare)
 // is queued for k_tile_clip -- the clip keeps it out of this loop's registers (occupancy: the
 // setup is memory-latency-bound).
+// (occupancy caps of 7 / 8 waves per SIMD, 72 / 64 VGPRs, measured slower: 580 -> 605 / 845 us, part 0
+// of 8 129 -> 171 / 218 us; profiles/r05_setup_occ_ab.txt)
 template <bool VS, bool CL>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, const uint32_t *__restrict__ cmap,

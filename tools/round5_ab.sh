@@ -35,6 +35,12 @@
 #             per-triangle depth cull (tzv4), occupancy caps 5 / 6 (o5 / o6 builds, S3R_TOCC)
 #   rasterocc fused raster occupancy caps 6 / 7 (to6 / to7), and 128-triangle stages for delivered frames
 #             at occupancy 6 (to6l128): stress N=1 / part 0 of 8, delivered and device bench lines
+#   setupocc  k_tile_setup occupancy caps 7 / 8 (so7 / so8 builds, S3R_SOCC)
+#   setupgrid tile-path kernels' workgroups per shard (S3R_TILE_GRID 1024 default / 256 / 24 / 16)
+#   fragocc   k_fragment's non-waterfall instance (2-chunk bins: 1080p, 4K / 8K parts) at occupancy 6
+#             (occ6 build: 80 VGPRs, 16 spilled) vs 5: every part of configs 3 and 4, 1080p bench lines
+#   stage192  the delivered frames' fused raster staging 192 triangles (tl192: 28.7 KB LDS, occupancy 5)
+#             instead of 256 (35.4 KB, occupancy 4)
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -188,6 +194,30 @@ rasterocc)
   for rep in 1 2; do
     BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'base stress||' 'to6 stress|build/librender_to6.so|' \
         'to6l128 stress|build/librender_to6l128.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
+setupocc)
+  S3R_LIB=build/librender_so8.so gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'base||' 'so7|build/librender_so7.so|' 'so8|build/librender_so8.so|' \
+      'base2||' 'so7b|build/librender_so7.so|' 'so8b|build/librender_so8.so|' 2>&1 | tee $OUT/ab.txt ;;
+setupgrid)
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1" bash tools/stress_lib_ab.sh 'g1024||' 'g256||S3R_TILE_GRID=256' 'g24||S3R_TILE_GRID=24' \
+      'g16||S3R_TILE_GRID=16' 'g1024b||' 'g256b||S3R_TILE_GRID=256' 2>&1 | tee $OUT/ab.txt ;;
+fragocc)
+  S3R_LIB=build/librender_occ6.so gpu_suite $OUT/parity.log tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
+  for tag in base occ6; do
+    lib=; [ $tag = occ6 ] && lib=build/librender_occ6.so
+    env ${lib:+S3R_LIB=$lib} timeout -k 10 600 python3 -u tools/parts_all.py --configs 3,4 --out $OUT/parts_$tag.jsonl > $OUT/parts_$tag.log 2>&1 || exit 1
+  done
+  BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'base 1080p||' 'occ6 1080p|build/librender_occ6.so|' \
+      'base2 1080p||' 'occ6b 1080p|build/librender_occ6.so|' 2>&1 | tee $OUT/ab.txt ;;
+stage192)
+  S3R_LIB=build/librender_tl192.so gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  for rep in 1 2; do
+    BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'base stress||' 'tl192 stress|build/librender_tl192.so|' \
+        2>&1 | tee -a $OUT/ab.txt || exit 1
   done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
