@@ -108,6 +108,25 @@ __device__ __forceinline__ float edge_fn(F3 a, F3 b, float cx, float cy) {
     return (cx - a.x) * (a.y - b.y) + (cy - a.y) * (b.x - a.x);     // EDGE_FUNCTION, render.cpp:9
 }
 
+// render.cpp:319-336: wstart at the bbox's first pixel centre and the per-pixel / per-row steps from the
+// three raster corners (x, y).  Shared by the setup and by the tile raster, which recomputes them from
+// the corners in its 48-B records (the same operations on the same operands: the same floats).
+__device__ __forceinline__ void raster_steps(F3 a, F3 b, F3 c, uint32_t xmin, uint32_t ymin, float *ws, float *dx,
+                                             float *dy) {
+    const float area = edge_fn(a, b, c.x, c.y);
+    const float ooa = 1 / area;
+    const float px = (float)xmin + 0.5f, py = (float)ymin + 0.5f;
+    ws[0] = edge_fn(b, c, px, py) * ooa;
+    ws[1] = edge_fn(c, a, px, py) * ooa;
+    ws[2] = edge_fn(a, b, px, py) * ooa;
+    dx[0] = (b.y - c.y) * ooa;
+    dx[1] = (c.y - a.y) * ooa;
+    dx[2] = (a.y - b.y) * ooa;
+    dy[0] = (c.x - b.x) * ooa;
+    dy[1] = (a.x - c.x) * ooa;
+    dy[2] = (b.x - a.x) * ooa;
+}
+
 // render.cpp:311-336, the position-only part of the setup: reject / cull (:312, :314, :317), bbox,
 // wstart, per-pixel and per-row steps, 1/z per corner.  False = no pixel of the frame.
 __device__ __forceinline__ bool raster_part(const Vert d[3], float sw, float sh, TriSetup &t) {
@@ -117,21 +136,11 @@ __device__ __forceinline__ bool raster_part(const Vert d[3], float sw, float sh,
     const float rny = fminf(fminf(d[0].rv.y, d[1].rv.y), d[2].rv.y);
     const float area = edge_fn(d[0].rv, d[1].rv, d[2].rv.x, d[2].rv.y);
     if (rmx < 0 || rmy < 0 || rnx >= sw || rny >= sh || area < 10) return false;   // :312, :314, :317
-    const float ooa = 1 / area;
     t.xmin = u32_of_float(fmaxf(0, rnx));
     t.xmax = u32_of_float(fminf(sw - 1, rmx));
     t.ymin = u32_of_float(fmaxf(0, rny));
     t.ymax = u32_of_float(fminf(sh - 1, rmy));
-    const float px = (float)t.xmin + 0.5f, py = (float)t.ymin + 0.5f;
-    t.ws[0] = edge_fn(d[1].rv, d[2].rv, px, py) * ooa;
-    t.ws[1] = edge_fn(d[2].rv, d[0].rv, px, py) * ooa;
-    t.ws[2] = edge_fn(d[0].rv, d[1].rv, px, py) * ooa;
-    t.dx[0] = (d[1].rv.y - d[2].rv.y) * ooa;
-    t.dx[1] = (d[2].rv.y - d[0].rv.y) * ooa;
-    t.dx[2] = (d[0].rv.y - d[1].rv.y) * ooa;
-    t.dy[0] = (d[2].rv.x - d[1].rv.x) * ooa;
-    t.dy[1] = (d[0].rv.x - d[2].rv.x) * ooa;
-    t.dy[2] = (d[1].rv.x - d[0].rv.x) * ooa;
+    raster_steps(d[0].rv, d[1].rv, d[2].rv, t.xmin, t.ymin, t.ws, t.dx, t.dy);
     t.ws[3] = t.dx[3] = t.dy[3] = t.rvz[3] = 0.0f;
 #pragma unroll
     for (int k = 0; k < 3; k++) t.rvz[k] = 1 / d[k].rv.z;
@@ -1426,14 +1435,15 @@ __device__ __forceinline__ uint32_t bucket_ceiling(uint32_t b) {
     return b == 0 ? 0xFFFFFFFFu : (kBucketTop - b + 1u) << 22;
 }
 
-struct alignas(16) RasterRec {                     // 64 B: one line per live slot
-    uint32_t bx, by, slot, zb;                     // bx = xmin | xmax << 16, by = ymin | ymax << 16,
-                                                   // zb = bits of ooz_bound() (hierarchical depth cull)
-    float ws[3], dx0;
-    float dx12[2], dy01[2];
-    float dy2, rz[3];
+// 48 B per live slot: the box, the depth bound, 1/z per corner and the three raster corners (x, y);
+// the raster and the resolve recompute wstart and the steps from the corners (raster_steps).
+struct alignas(16) RasterRec {
+    uint32_t bx, by, zb;                           // bx = xmin | xmax << 16, by = ymin | ymax << 16,
+    float rz0;                                     // zb = bits of ooz_bound() (hierarchical depth cull)
+    float rz1, rz2, x0, y0;
+    float x1, y1, x2, y2;
 };
-static_assert(sizeof(RasterRec) == 64, "RasterRec layout");
+static_assert(sizeof(RasterRec) == 48, "RasterRec layout");
 
 // The corner's camera-space and raster position (render.cpp:286, :288).  The two projections share
 // one refined reciprocal of -cv.z where the trimmed division is exact (div_in_range, s3r_common.h);
@@ -1630,19 +1640,15 @@ S3R_HD float ooz_bound(const TriSetup &t) {
     return is_finite(b) && rmax > 0.0f && asum > 0.0f ? b : __builtin_inff();
 }
 
-// The live slot's raster record, stored non-temporal: the records (~10 M x 64 B on the stress
+// The live slot's raster record (emit_slot) is stored non-temporal: the records (~10 M on the stress
 // scene) stream out past the setup's index / vertex loads instead of occupying L2 until the raster
-// reads them.  Stress scene, one MI355X, same box (profiles/r05_ntrec_ab.txt): setup 608-610 ->
-// 577 us serialised, part 0 of 8 5 829-5 932 -> 6 283 fps, whole frame 979-993 -> 1 007 fps; the
-// bin entries stored the same way measured slower (624 us: the raster reads them back soon).
+// reads them.  Stress scene, one MI355X, same box (profiles/r05_ntrec_ab.txt, 64-B records then): setup
+// 608-610 -> 577 us serialised, part 0 of 8 5 829-5 932 -> 6 283 fps, whole frame 979-993 -> 1 007 fps;
+// the bin entries stored the same way measured slower (624 us: the raster reads them back soon).
+// 48-B records (the corners instead of wstart and the steps, recomputed by raster_steps where read):
+// setup 580 -> 539-545 us, raster 430 -> 420 us, whole frame pipelined 1 050 -> 1 107-1 113 fps
+// (profiles/r05_rec48_ab.txt).
 typedef float nt_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void write_rec(RasterRec *__restrict__ r, const TriSetup &t, uint32_t slot, uint32_t zb) {
-    nt_f4 *q = reinterpret_cast<nt_f4 *>(r);
-    __builtin_nontemporal_store((nt_f4){u2f(t.xmin | (t.xmax << 16)), u2f(t.ymin | (t.ymax << 16)), u2f(slot), u2f(zb)}, q);
-    __builtin_nontemporal_store((nt_f4){t.ws[0], t.ws[1], t.ws[2], t.dx[0]}, q + 1);
-    __builtin_nontemporal_store((nt_f4){t.dx[1], t.dx[2], t.dy[0], t.dy[1]}, q + 2);
-    __builtin_nontemporal_store((nt_f4){t.dy[2], t.rvz[0], t.rvz[1], t.rvz[2]}, q + 3);
-}
 
 // Vertex stage (render.cpp:285-289 as a pass over the vertex stream, north_star's "vertex-stage
 // kernel"; S3R_VERTEX_STAGE=1): every vertex transformed and projected once, coalesced, into
@@ -1772,26 +1778,26 @@ __device__ __forceinline__ void wave_append_u32(bool want, uint32_t v, uint32_t 
 // entry append and the counting are wave-aggregated).
 // Bins mode (tbin non-null, kernels.hip "bins"): the slot goes straight into the fixed-capacity
 // bins of its (tile, bucket)s -- no live entry, no fill pass.
-__device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, uint32_t slot, uint32_t band, uint32_t nparts,
-                                          uint32_t part, uint32_t tiles_x, uint32_t xoff, RasterRec *__restrict__ recs,
-                                          uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
+__device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const Vert *dv, uint32_t slot, uint32_t band,
+                                          uint32_t nparts, uint32_t part, uint32_t tiles_x, uint32_t xoff,
+                                          RasterRec *__restrict__ recs, uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
                                           uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin = nullptr,
                                           uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr) {
     uint32_t bx = kDeadBox, by = 0;
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
-        const uint32_t zb = f2u(ooz_bound(ts));
-        const uint32_t bt = tile_box(ts.xmin | (ts.xmax << 16), zb, xoff);
-        sp = box_tiles(bt, ts.ymin | (ts.ymax << 16), band, nparts, part);
+        // the span first (it does not depend on the depth bucket) and the corners stored before the
+        // depth bound is computed: they are dead by then (fewer registers at ooz_bound's peak)
+        sp = box_tiles(tile_box(ts.xmin | (ts.xmax << 16), 0u, xoff), ts.ymin | (ts.ymax << 16), band, nparts, part);
         if (sp.n) {
-            bx = bt;
+            nt_f4 *q = reinterpret_cast<nt_f4 *>(recs + slot);
+            __builtin_nontemporal_store((nt_f4){ts.rvz[1], ts.rvz[2], dv[0].rv.x, dv[0].rv.y}, q + 1);
+            __builtin_nontemporal_store((nt_f4){dv[1].rv.x, dv[1].rv.y, dv[2].rv.x, dv[2].rv.y}, q + 2);
+            const uint32_t zb = f2u(ooz_bound(ts));
+            bx = tile_box(ts.xmin | (ts.xmax << 16), zb, xoff);
             by = ts.ymin | (ts.ymax << 16);
-#if defined(S3R_TABLATE) && (S3R_TABLATE & 32)
-            // ablation (wrong pixels, bounded work): only the record's first 16 B (box, slot, bound)
-            reinterpret_cast<uint4 *>(recs + slot)[0] = make_uint4(ts.xmin | (ts.xmax << 16), ts.ymin | (ts.ymax << 16), slot, zb);
-#else
-            write_rec(recs + slot, ts, slot, zb);
-#endif
+            sp.bucket = bx >> 24;
+            __builtin_nontemporal_store((nt_f4){u2f(ts.xmin | (ts.xmax << 16)), u2f(by), u2f(zb), ts.rvz[0]}, q);
         }
     }
     if (tbin) {
@@ -1889,7 +1895,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -1916,7 +1922,7 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
     const float half_w = sw / 2, half_h = sh / 2;
     for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += per * 256u) {   // wave-uniform
         const uint32_t j = j0 + lane;
-        Vert d[3];
+        Vert d[3], app[3];
         TriSetup ts, ta;
         bool live_t = false, live_a = false;
         uint32_t t = 0;
@@ -1932,13 +1938,12 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
                 d[k].n = mk3(0, 0, 0);
                 d[k].pay = make_float4(0, 0, 0, 0);
             }
-            Vert app[3];
             uint32_t app_first = 0;
             if (clip_tri(d, app, &app_first, false, factor, half_w, half_h)) live_a = raster_part(app, sw, sh, ta);
             live_t = raster_part(d, sw, sh, ts);
         }
-        emit_slot(live_a, ta, ntri + t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
-        emit_slot(live_t, ts, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_a, ta, app, ntri + t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
     }
 }
 
@@ -2096,11 +2101,16 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
     const float ooz = u2f((uint32_t)(k >> 32));
     if (DEFER && s >= sc.ntri) return kDeferPixel;
     const float4 *q = reinterpret_cast<const float4 *>(sc.recs + s);
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-    const uint32_t xmin = f2u(q0.x) & 0xFFFFu, ymin = f2u(q0.y) & 0xFFFFu;
-    const float w0 = short_walk(short_walk(q1.x, q2.z, y - ymin), q1.w, x - xmin);
-    const float w1 = short_walk(short_walk(q1.y, q2.w, y - ymin), q2.x, x - xmin);
-    const float w2 = short_walk(short_walk(q1.z, q3.x, y - ymin), q2.y, x - xmin);
+    const uint32_t xmin = f2u(q[0].x) & 0xFFFFu, ymin = f2u(q[0].y) & 0xFFFFu;
+    float rws[3], rdx[3], rdy[3], rrz[3];
+    {
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+        raster_steps(mk3(q1.z, q1.w, 0.0f), mk3(q2.x, q2.y, 0.0f), mk3(q2.z, q2.w, 0.0f), xmin, ymin, rws, rdx, rdy);
+        rrz[0] = q0.w; rrz[1] = q1.x; rrz[2] = q1.y;
+    }
+    const float w0 = short_walk(short_walk(rws[0], rdy[0], y - ymin), rdx[0], x - xmin);
+    const float w1 = short_walk(short_walk(rws[1], rdy[1], y - ymin), rdx[1], x - xmin);
+    const float w2 = short_walk(short_walk(rws[2], rdy[2], y - ymin), rdx[2], x - xmin);
     TriSetup ts;
     const uint32_t t = s < sc.ntri ? s : s - sc.ntri;
     Vert d[3];
@@ -2121,9 +2131,8 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
         slot_setup(s, sc.ntri, sc.vtx, sc.nrm, sc.pay, sc.disc, sc.vidx, sc.aidx, sc.m, sc.factor, sc.sw, sc.sh, ts);
     } else {
         ts.kind = kDead;
-        ts.rvz[0] = q3.y; ts.rvz[1] = q3.z; ts.rvz[2] = q3.w;
-        ts.dx[0] = q1.w; ts.dx[1] = q2.x; ts.dx[2] = q2.y;
-        ts.dy[0] = q2.z; ts.dy[1] = q2.w; ts.dy[2] = q3.x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) { ts.rvz[c] = rrz[c]; ts.dx[c] = rdx[c]; ts.dy[c] = rdy[c]; }
         shading_part(d, sc.disc[sc.aidx[3 * t]] != 0, ts);
     }
     return shade(&ts, w0, w1, w2, ooz, sc.tex, sc.ntex);
@@ -2142,7 +2151,7 @@ template <uint32_t STAGE = kTileStage>
                                        // (profiles/r05_raster_occ_ab.txt): raster 462 -> 430 us serialised, whole
                                        // frame pipelined 1 030-1 036 -> 1 068-1 083 fps; 7 (72 VGPRs, 12 spilled):
                                        // the same raster time, part 0 of 8 -2.5 %
-__global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
+__global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_tile_raster(
     const RasterRec *__restrict__ recs, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
     uint32_t tiles_x, const uint32_t *__restrict__ offs, uint32_t *__restrict__ ctr,
     const uint32_t *__restrict__ list, uint32_t cap,
@@ -2200,7 +2209,7 @@ __global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
     // software pipeline: stage c0 + STAGE's list entries and records are loaded into registers
     // while stage c0's items run
     uint32_t s_nx = 0;
-    float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n, q3n = q0n;
+    float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n;
     auto fetch = [&](uint32_t c) {
         if (tid < STAGE && c + tid < n) {
             if (bin_cap) {
@@ -2227,7 +2236,7 @@ __global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
             }
 #endif
             const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
-            q0n = q[0]; q1n = q[1]; q2n = q[2]; q3n = q[3];
+            q0n = q[0]; q1n = q[1]; q2n = q[2];
         }
     };
     fetch(0);
@@ -2273,8 +2282,9 @@ __global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
         uint32_t nr = 0;
         if (tid < STAGE && j < n) {
             const uint32_t s = s_nx;
-            const float4 q0 = q0n, q1 = q1n, q2 = q2n, q3 = q3n;
+            const float4 q0 = q0n, q1 = q1n, q2 = q2n;
             const uint32_t bx = f2u(q0.x), by = f2u(q0.y);
+            const uint32_t zbits = f2u(q0.z);
             uint32_t lo = 1u, hi = 0u;
             local_row_range(by & 0xFFFFu, by >> 16, band, nparts, part, lo, hi);
             const uint32_t a = max(lo, tr0), b = min(hi, tr1);
@@ -2287,7 +2297,7 @@ __global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
 #endif
             if (nr && c0 > 0) {
                 const uint32_t g0 = (max(bx & 0xFFFFu, lx0) - lx0) >> 4, g1 = (min(bx >> 16, lx1) - lx0) >> 4;
-                const uint32_t zb = f2u(q0.w);
+                const uint32_t zb = zbits;
                 bool cull = true;
                 for (uint32_t r = a; r <= b && cull; r++)
                     for (uint32_t g = g0; g <= g1; g++) cull = cull && zb < ls.zmin[r - tr0][g];
@@ -2299,10 +2309,14 @@ __global__ void __launch_bounds__(kTileThreads, S3R_TOCC) k_tile_raster(
 #endif
             ls.slot[tid] = s; ls.xmin[tid] = bx & 0xFFFFu; ls.xmax[tid] = bx >> 16; ls.ymin[tid] = by & 0xFFFFu;
             ls.r0[tid] = a;
-            ls.ws[0][tid] = q1.x; ls.ws[1][tid] = q1.y; ls.ws[2][tid] = q1.z;
-            ls.dx[0][tid] = q1.w; ls.dx[1][tid] = q2.x; ls.dx[2][tid] = q2.y;
-            ls.dy[0][tid] = q2.z; ls.dy[1][tid] = q2.w; ls.dy[2][tid] = q3.x;
-            ls.rz[0][tid] = q3.y; ls.rz[1][tid] = q3.z; ls.rz[2][tid] = q3.w;
+            if (nr) {                                    // (the steps only for a triangle with rows here)
+                float ws[3], dx[3], dy[3];
+                raster_steps(mk3(q1.z, q1.w, 0.0f), mk3(q2.x, q2.y, 0.0f), mk3(q2.z, q2.w, 0.0f), bx & 0xFFFFu,
+                             by & 0xFFFFu, ws, dx, dy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) { ls.ws[c][tid] = ws[c]; ls.dx[c][tid] = dx[c]; ls.dy[c][tid] = dy[c]; }
+            }
+            ls.rz[0][tid] = q0.w; ls.rz[1][tid] = q1.x; ls.rz[2][tid] = q1.y;
         }
         fetch(c0 + STAGE);
         // exclusive scan of the row counts over the stage (wave shuffles + wave totals)

@@ -41,6 +41,10 @@
 #             (occ6 build: 80 VGPRs, 16 spilled) vs 5: every part of configs 3 and 4, 1080p bench lines
 #   stage192  the delivered frames' fused raster staging 192 triangles (tl192: 28.7 KB LDS, occupancy 5)
 #             instead of 256 (35.4 KB, occupancy 4)
+#   rec48     48-B raster records (box, bound, 1/z, the three raster corners; the raster and the resolve
+#             recompute wstart and the steps: rec48 build, S3R_REC48) vs the 64-B records (product)
+#   rec48s6   the 48-B records with k_tile_setup capped at 80 VGPRs (occupancy 6, as the 64-B build had)
+#   rec48b    the 48-B records again, the corners stored before the depth bound (fewer live registers)
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -217,6 +221,43 @@ stage192)
   stress_data || exit 1
   for rep in 1 2; do
     BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'base stress||' 'tl192 stress|build/librender_tl192.so|' \
+        2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
+rec48)
+  S3R_LIB=build/librender_rec48.so gpu_suite $OUT/tiles.log tests/test_tiles.py tests/test_multi_device.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'rec64||' 'rec48|build/librender_rec48.so|' 'rec64b||' \
+      'rec48b|build/librender_rec48.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'rec64 stress||' 'rec48 stress|build/librender_rec48.so|' \
+      'rec64b stress||' 'rec48b stress|build/librender_rec48.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  for spec in 'rec64|' 'rec48|build/librender_rec48.so'; do
+    IFS='|' read -r tag lib <<< "$spec"
+    for c in FETCH_SIZE WRITE_SIZE; do
+      env S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$PWD/$OUT/pmc_${tag}_$c" -o run -- \
+          python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $D --steps 10 > $OUT/pmc_${tag}_$c.log 2>&1 || { tail -5 $OUT/pmc_${tag}_$c.log; exit 1; }
+    done
+    python3 tools/pmc_summary.py $OUT --last 10 > /dev/null 2>&1 || true
+    find $OUT -name '*kernel_trace.csv' -delete
+  done
+  for spec in rec64 rec48; do
+    python3 tools/pmc_summary.py $OUT/pmc_${spec}_FETCH_SIZE --last 10 > $OUT/pmcf_$spec.txt 2>&1 || true
+    python3 tools/pmc_summary.py $OUT/pmc_${spec}_WRITE_SIZE --last 10 > $OUT/pmcw_$spec.txt 2>&1 || true
+  done
+  find $OUT -name '*.csv' -size +5M -delete ;;
+rec48s6)
+  S3R_LIB=build/librender_rec48s6.so gpu_suite $OUT/tiles.log tests/test_tiles.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'rec64||' 'rec48|build/librender_rec48.so|' 'rec48s6|build/librender_rec48s6.so|' \
+      'rec64b||' 'rec48s6b|build/librender_rec48s6.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'rec64 stress||' 'rec48s6 stress|build/librender_rec48s6.so|' \
+      2>&1 | tee -a $OUT/ab.txt ;;
+rec48b)
+  S3R_LIB=build/librender_rec48.so gpu_suite $OUT/tiles.log tests/test_tiles.py tests/test_multi_device.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'rec64||' 'rec48|build/librender_rec48.so|' 'rec64b||' \
+      'rec48b|build/librender_rec48.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  for rep in 1 2; do
+    BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'rec64 stress||' 'rec48 stress|build/librender_rec48.so|' \
         2>&1 | tee -a $OUT/ab.txt || exit 1
   done ;;
 *)
