@@ -45,6 +45,7 @@
 #             recompute wstart and the steps: rec48 build, S3R_REC48) vs the 64-B records (product)
 #   rec48s6   the 48-B records with k_tile_setup capped at 80 VGPRs (occupancy 6, as the 64-B build had)
 #   rec48b    the 48-B records again, the corners stored before the depth bound (fewer live registers)
+#   clshallow frame parts' setup (clusters) one deep again (product) vs two deep (prev build)
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -259,6 +260,14 @@ rec48b)
   for rep in 1 2; do
     BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'rec64 stress||' 'rec48 stress|build/librender_rec48.so|' \
         2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
+clshallow)
+  gpu_suite $OUT/tiles.log tests/test_tiles.py tests/test_multi_device.py || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="8" bash tools/stress_lib_ab.sh 'shallow||' 'deep|build/librender_prev.so|' 'shallow2||' \
+      'deep2|build/librender_prev.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  for n in 2 4; do
+    NS="$n" bash tools/stress_lib_ab.sh 'shallow||' 'deep|build/librender_prev.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
   done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
