@@ -46,6 +46,8 @@
 #   rec48s6   the 48-B records with k_tile_setup capped at 80 VGPRs (occupancy 6, as the 64-B build had)
 #   rec48b    the 48-B records again, the corners stored before the depth bound (fewer live registers)
 #   clshallow frame parts' setup (clusters) one deep again (product) vs two deep (prev build)
+#   linfast   k_fragment: triangles whose three components are exactly linear over the chunk skip the
+#             table fill (values c + k delta where read; linf build, S3R_LINFAST) vs every chunk tabled
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -269,6 +271,15 @@ clshallow)
   for n in 2 4; do
     NS="$n" bash tools/stress_lib_ab.sh 'shallow||' 'deep|build/librender_prev.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
   done ;;
+linfast)
+  S3R_LIB=build/librender_linf.so gpu_suite $OUT/parity.log tests/test_gpu_parity.py tests/test_multi_device.py tests/test_host_loop.py \
+      tests/test_multi.py tests/test_stream_order.py || exit 1
+  for rep in 1 2; do
+    PARTS8=1 bash tools/lib_ab.sh 'base||' 'linf|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'base P_id||' 'linf P_id|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--width 7680 --height 4320' bash tools/lib_ab.sh 'base 8K||' 'linf 8K|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'base 1080p||' 'linf 1080p|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
