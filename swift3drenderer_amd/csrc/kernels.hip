@@ -599,6 +599,19 @@ __device__ void publish_sky_flags(const SkyFlags &sf, const uint32_t *__restrict
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the k-th set bit of the host's slot mask (wave-uniform: scalar loads of the kernel argument)
+__device__ __forceinline__ uint32_t live_slot(const SlotMask &m, uint32_t k) {
+    uint32_t w = 0;
+    for (; w + 1 < kLiveMaskSlots / 64; w++) {
+        const uint32_t c = (uint32_t)__popcll(m.bits[w]);
+        if (k < c) break;
+        k -= c;
+    }
+    uint64_t b = m.bits[w];
+    for (; k; k--) b &= b - 1ull;
+    return w * 64u + (uint32_t)__builtin_ctzll(b);
+}
+
 __device__ __forceinline__ void geo_arrive(const SkyFlags &sf, uint32_t rb) {
     if (sf.flags && threadIdx.x == 0) atomicAdd(sf.geo_cnt + rb * kGeoCntStride, 1u);
 }
@@ -633,7 +646,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     uint32_t rows_local, uint32_t segs, uint32_t segw, TriSetup *__restrict__ tris,
     float *__restrict__ rowtab, uint32_t *__restrict__ bincnt, uint4 *__restrict__ pairs,
     uint32_t nbins, uint32_t *__restrict__ order, uint32_t nrb, SkyFlags sky, uint32_t row_starts,
-    uint32_t nslots) {
+    uint32_t nslots, SlotMask live) {
     __shared__ TriSetup sts;
     extern __shared__ uint8_t posmap[];        // per bin of this workgroup: its pair index, 0xFF = none
     // slot-major 1-D grid: workgroup 0 (with `order`) computes this frame's fragment order, then the
@@ -646,12 +659,20 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
         order_bins(order + nbins, nbins, order);
         return;
     }
-    const uint32_t pub0 = order ? 1u : 0u, first = pub0 + (sky.flags ? nrb : 0u);   // publishers, geometry
-    if (sky.flags && g0 < first) {
-        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, nslots);
+    // publishers, the dead-slot marker (host cull), geometry
+    const uint32_t pub0 = order ? 1u : 0u, mark0 = pub0 + (sky.flags ? nrb : 0u), first = mark0 + live.on;
+    if (sky.flags && g0 < mark0) {
+        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, live.on ? live.nlive : nslots);
         return;
     }
-    const uint32_t tid = threadIdx.x, gs = g0 - first, slot = gs / nrb, rb = gs - slot * nrb;
+    if (live.on && g0 == mark0) {
+        // the slots the host culled, and every clip slot (none launched with the mask): dead
+        for (uint32_t s = threadIdx.x; s < ntri; s += blockDim.x)
+            if (!((live.bits[s >> 6] >> (s & 63u)) & 1ull)) tris[s].kind = tris[ntri + s].kind = kDead;
+        return;
+    }
+    const uint32_t tid = threadIdx.x, gs = g0 - first, gk = gs / nrb, rb = gs - gk * nrb;
+    const uint32_t slot = live.on ? live_slot(live, gk) : gk;
 #ifdef S3R_STATS
     const unsigned long long t_start = wall_clock64();
     if (tid == 0) atomicMin(&g_tstats[2], t_start);
@@ -2686,18 +2707,23 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
-                     uint32_t *order, const GeoSkyFlags *gsf, bool row_starts, bool clip_slots) {
+                     uint32_t *order, const GeoSkyFlags *gsf, bool row_starts, bool clip_slots,
+                     const SlotMask *live) {
+    const bool masked = live && live->on && !clip_slots && ntri <= kLiveMaskSlots;
     const uint32_t nslots = clip_slots ? 2u * ntri : ntri;
+    SlotMask lm{};
+    if (masked) lm = *live;
     const uint32_t nrb = (rows_local + kGeoRows - 1) / kGeoRows;
+    const uint32_t nwg = (masked ? lm.nlive : nslots) * nrb + (masked ? 1u : 0u);   // + the dead-slot marker
     if (ntri == 0 || rows_local == 0 || (gsf && nrb > kGeoCntMax)) {
         // nothing to set up (every bin is sky), or more row blocks than counters: k_sky_flags publishes
         if (ntri && rows_local) {
             const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-            { hipExtLaunchKernelGGL(k_geometry, dim3(nslots * nrb + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
+            { hipExtLaunchKernelGGL(k_geometry, dim3(nwg + (order ? 1u : 0u)), dim3(3 * kGeoRows), posmap_bytes,
                                   st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
                                   nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
                                   (uint32_t)fragment_bins(W, rows_local), order, nrb,
-                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u, nslots); after_launch("k_geometry", st); }
+                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u, nslots, lm); after_launch("k_geometry", st); }
         }
         if (gsf)
             launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
@@ -2711,10 +2737,10 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;
-    { hipExtLaunchKernelGGL(k_geometry, dim3(nslots * nrb + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
+    { hipExtLaunchKernelGGL(k_geometry, dim3(nwg + (order ? 1u : 0u) + (gsf ? nrb : 0u)),
                           dim3(3 * kGeoRows), posmap_bytes, st, nullptr, done, 0, vtx, nrm, pay, disc, vidx, aidx, ntri,
                           m, factor, W, H, band, nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt,
-                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u, nslots); after_launch("k_geometry", st); }
+                          pairs, (uint32_t)fragment_bins(W, rows_local), order, nrb, sky, row_starts ? 1u : 0u, nslots, lm); after_launch("k_geometry", st); }
 }
 
 void launch_fragment(const TriSetup *tris, uint32_t nslots, const float *rowtab, const uint32_t *tex, uint32_t ntex,

@@ -337,6 +337,8 @@ struct Lib {
     std::vector<uint32_t> near_vidx;
     std::vector<uint8_t> near_side;
     bool clip_slots = true;                    // this frame: launch k_geometry's clip-appended slots
+    SlotMask live{};                           // this frame: the slots k_geometry launches (cull_slots)
+    std::vector<double> near_rv;               // per vertex: screen x, y and their error bound (cull_slots)
     bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
     bool clusters_whole = false;               // ... also for whole frames (S3R_CLUSTERS=2)
     int raster_path = 0;                       // 0 auto, 1 rows (k_geometry + k_fragment), 2 tiles
@@ -383,7 +385,7 @@ struct Lib {
     uintptr_t unmapped_a = 0;
     uint64_t unmapped_epoch = 0;
     // environment switches read once per library state (release_all resets them: a configure re-reads)
-    int env_row_starts = -1, env_host_uncached = -1;
+    int env_row_starts = -1, env_host_uncached = -1, env_slot_cull = -1;
     // fill-thread placement: frames in a row whose buffer sat on another node than the placement's
     int fill_node_streak = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
@@ -740,6 +742,7 @@ void release_all() {
 }
 
 bool near_plane_crossing();
+void cull_slots(uint32_t W, uint32_t H);
 
 // render.cpp:266-280: first-call init, camera, resize.
 void frame_begin(const Input *input, uint32_t width, uint32_t height) {
@@ -758,6 +761,8 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
         unregister_all();
     }
     g.clip_slots = near_plane_crossing();
+    g.live.on = 0;
+    if (!g.clip_slots && env_on(g.env_slot_cull, "S3R_SLOT_CULL")) cull_slots(width, height);
 }
 
 TimingSlot *timing_slot(Dev &d) {
@@ -868,6 +873,63 @@ bool near_plane_crossing() {
         if (m == 3u) return true;
     }
     return false;
+}
+
+// Host slot cull, frames without clip slots (near_plane_crossing false: each triangle wholly in front
+// of the near plane or wholly behind it): slot t (original triangle t) is launched unless its setup
+// surely rejects it -- every corner behind the plane (render.cpp:306), or the triangle off the frame
+// or of area < 10 (:312, :314, :317: back faces included).  The host projects the corners in double
+// and widens each test by a bound on the device's float rounding (1e-6 of every summed term's
+// magnitude, four times float's worst case, carried through the divide and the area): a triangle
+// within that bound of a test stays launched, and the device decides it exactly.  k_geometry starts
+// no workgroup for a culled slot; one marker workgroup stores it dead (launch_geometry live).
+void cull_slots(uint32_t W, uint32_t H) {
+    if (g.ntri > kLiveMaskSlots || g.near_vidx.size() != 3 * (size_t)g.ntri) return;
+    const size_t nv = g.near_vtx.size();
+    g.near_rv.resize(3 * nv);
+    const double f = g.factor, hw = (double)((float)W / 2), hh = (double)((float)H / 2);
+    for (size_t i = 0; i < nv; i++) {
+        if (g.near_side[i] != 1u) continue;                  // behind the plane: no projection
+        const float4 v = g.near_vtx[i];
+        double c[3], sum[3];
+        for (int r = 0; r < 3; r++) {
+            const float *m = g.m.m[r];
+            const double a = (double)m[0] * v.x, b = (double)m[1] * v.y, e = (double)m[2] * v.z, h = (double)m[3] * v.w;
+            c[r] = ((a + b) + e) + h;
+            sum[r] = fabs(a) + fabs(b) + fabs(e) + fabs(h);
+        }
+        const double nz = -c[2], dz = 1e-6 * sum[2];
+        const double qx = c[0] * f / nz, qy = -c[1] * f / nz;
+        const double ex = f * (1e-6 * sum[0] + fabs(c[0]) * dz / nz) / nz + 1e-6 * (fabs(qx) + hw);
+        const double ey = f * (1e-6 * sum[1] + fabs(c[1]) * dz / nz) / nz + 1e-6 * (fabs(qy) + hh);
+        g.near_rv[3 * i] = qx + hw;
+        g.near_rv[3 * i + 1] = qy + hh;
+        g.near_rv[3 * i + 2] = ex > ey ? ex : ey;
+    }
+    SlotMask &lm = g.live;
+    memset(lm.bits, 0, sizeof(lm.bits));
+    lm.nlive = 0;
+    const double sw = W, sh = H;
+    for (uint32_t t = 0; t < g.ntri; t++) {
+        const uint32_t *vi = &g.near_vidx[3 * (size_t)t];
+        const uint8_t side = g.near_side[vi[0]] | g.near_side[vi[1]] | g.near_side[vi[2]];
+        if (side == 2u) continue;                            // :306
+        bool live = side != 1u;
+        if (!live) {
+            const double *a = &g.near_rv[3 * (size_t)vi[0]], *b = &g.near_rv[3 * (size_t)vi[1]],
+                         *c = &g.near_rv[3 * (size_t)vi[2]];
+            const double E = std::max(std::max(a[2], b[2]), c[2]);
+            const double rmx = std::max(std::max(a[0], b[0]), c[0]), rnx = std::min(std::min(a[0], b[0]), c[0]);
+            const double rmy = std::max(std::max(a[1], b[1]), c[1]), rny = std::min(std::min(a[1], b[1]), c[1]);
+            const double t1 = (c[0] - a[0]) * (a[1] - b[1]), t2 = (c[1] - a[1]) * (b[0] - a[0]);
+            const double aerr = 2 * E * (fabs(a[1] - b[1]) + fabs(c[0] - a[0]) + fabs(c[1] - a[1]) + fabs(b[0] - a[0])) +
+                                8 * E * E + 1e-6 * (fabs(t1) + fabs(t2));
+            const bool off = rmx < -E || rmy < -E || rnx >= sw + E || rny >= sh + E;
+            live = !off && t1 + t2 + aerr >= 10 && std::isfinite(E) && std::isfinite(t1 + t2 + aerr);
+        }
+        if (live) { lm.bits[t >> 6] |= 1ull << (t & 63u); lm.nlive++; }
+    }
+    lm.on = 1;
 }
 
 bool use_tile_path() {
@@ -1339,7 +1401,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     }
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
-                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts, g.clip_slots);
+                    lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts, g.clip_slots, &g.live);
     d.hp.lap(3);
     if (ts) HIPCHECK(hipEventRecord(ts->geo1, geo));
     // fragment on the caller's stream, after the previous frame and this frame's geometry; its first

@@ -63,12 +63,21 @@ struct GeoSkyFlags {
 // clip_slots = false: no triangle can cross the near plane this frame (the host's check,
 // render_api.cpp near_plane_crossing), so the launch leaves out the clip-appended slots T..2T-1 (their
 // records are marked dead) -- half the workgroups, one dispatch round fewer for small scenes.
+// Host slot cull (render_api.cpp cull_slots): with `live`, k_geometry starts workgroups only for the
+// original slots whose bit is set (frames without clip slots, scenes up to kLiveMaskSlots triangles);
+// one extra workgroup marks every other slot dead.
+constexpr uint32_t kLiveMaskSlots = 1024;
+struct SlotMask {
+    uint64_t bits[kLiveMaskSlots / 64];
+    uint32_t nlive;                    // set bits
+    uint32_t on;                       // 0: every slot launched (bits unused)
+};
 void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, const uint8_t *disc,
                      const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri, const Mat34 &m, float factor,
                      uint32_t W, uint32_t H, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                      TriSetup *tris, float *rowtab, uint32_t *bincnt, uint4 *pairs, hipStream_t st, hipEvent_t done,
                      uint32_t *order, const GeoSkyFlags *gsf = nullptr, bool row_starts = false,
-                     bool clip_slots = true);
+                     bool clip_slots = true, const SlotMask *live = nullptr);
 uint32_t fragment_segments(uint32_t W);
 
 uint32_t fragment_segment_pixels();

@@ -67,6 +67,23 @@ def test_clip_slots_follow_the_near_plane(gpu_renderer, scene_dir):
         assert np.array_equal(got, want), (pose, diff_report(got, want))
 
 
+def test_slot_cull_turning_camera(gpu_renderer, scene_dir):
+    """k_geometry launches only the slots the host does not surely reject (render_api.cpp cull_slots:
+    behind the near plane, off the frame, back faces and slivers of area < 10, render.cpp:306-317): the
+    camera turns through a full circle and pitches, so triangles leave the frame on every side and turn
+    their backs, each frame against the oracle (tiny and wide frames too)."""
+    from oracle.oracle import OracleRenderer
+    for name, w, h in [('full', 320, 240), ('regular', 256, 96), ('full', 33, 7)]:
+        path = scene_dir[name]
+        o = OracleRenderer(path)
+        gpu_renderer.configure(path)
+        for k in range(30):
+            inp = (0, 0, 0, 0, 24.0 * k, 40.0 * np.sin(k / 3.0))
+            want = o.update_and_render(w, h, inp)
+            got = gpu_renderer.update_and_render(w, h, inp)
+            assert np.array_equal(got, want), f'{name} {w}x{h} frame {k} {inp}: ' + diff_report(got, want)
+
+
 def test_resize_between_calls(gpu_renderer, scene_dir):
     """render.cpp:275-280: factor changes only when W*H changes; camera state carries over."""
     from oracle.oracle import OracleRenderer

@@ -48,6 +48,11 @@
 #   clshallow frame parts' setup (clusters) one deep again (product) vs two deep (prev build)
 #   linfast   k_fragment: triangles whose three components are exactly linear over the chunk skip the
 #             table fill (values c + k delta where read; linf build, S3R_LINFAST) vs every chunk tabled
+#   slotcull  k_geometry launching only the slots the host's cull keeps (product) vs every slot
+#             (S3R_SLOT_CULL=0): parity suites, 4K / P_id / 8K / 1080p bench lines, geometry timelines
+#   slotcull2 the same, device and delivered rates only, three alternating repetitions, overhead probes
+#   slotcull3 1080p delivered frames, the variants in the other order
+#                                                                   -> r05_slot_cull_ab.txt
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
 set -o pipefail
@@ -280,6 +285,36 @@ linfast)
   BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'base P_id||' 'linf P_id|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
   BENCH_EXTRA='--width 7680 --height 4320' bash tools/lib_ab.sh 'base 8K||' 'linf 8K|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
   BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'base 1080p||' 'linf 1080p|build/librender_linf.so|' 2>&1 | tee -a $OUT/ab.txt ;;
+slotcull)
+  gpu_suite $OUT/parity.log tests/test_gpu_parity.py tests/test_host_loop.py tests/test_multi_device.py tests/test_multi.py \
+      tests/test_abi.py tests/test_stream_order.py || exit 1
+  for rep in 1 2; do
+    PARTS8=1 bash tools/lib_ab.sh 'cull||' 'nocull||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'cull P_id||' 'nocull P_id||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--width 7680 --height 4320' bash tools/lib_ab.sh 'cull 8K||' 'nocull 8K||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'cull 1080p||' 'nocull 1080p||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  timeout -k 10 180 python3 tools/geo_timeline.py --delivered > $OUT/geo_delivered.txt 2>&1 || exit 1
+  S3R_SLOT_CULL=0 timeout -k 10 180 python3 tools/geo_timeline.py --delivered > $OUT/geo_delivered_nocull.txt 2>&1 ;;
+slotcull2)
+  for rep in 1 2 3; do
+    bash tools/lib_ab.sh 'cull||' 'nocull||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+    BENCH_EXTRA='--pose P_id' bash tools/lib_ab.sh 'cull P_id||' 'nocull P_id||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+    BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'cull 1080p||' 'nocull 1080p||S3R_SLOT_CULL=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  for rep in 1 2; do
+    for spec in "cull|" "nocull|S3R_SLOT_CULL=0"; do
+      IFS='|' read -r tag envs <<< "$spec"
+      probe $tag $envs -- --steps 2000 | tee -a $OUT/probe.txt || exit 1
+    done
+  done ;;
+slotcull3)
+  for rep in 1 2 3 4; do
+    BENCH_EXTRA='--scene flat --width 1920 --height 1080' bash tools/lib_ab.sh 'nocull 1080p||S3R_SLOT_CULL=0' 'cull 1080p||' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  for rep in 1 2; do
+    BENCH_EXTRA='--scene full --width 1920 --height 1080' bash tools/lib_ab.sh 'nocull full1080||S3R_SLOT_CULL=0' 'cull full1080||' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
 esac
