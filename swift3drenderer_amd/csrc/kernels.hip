@@ -1466,6 +1466,14 @@ struct alignas(16) RasterRec {
 };
 static_assert(sizeof(RasterRec) == 48, "RasterRec layout");
 
+// A bin / list entry is a slot, | kNoRecBit when the slot has no raster record.  With NOREC
+// (k_tile_setup; delivered frames) the setup writes no record for a slot the raster can set up again
+// from the scene -- an original triangle wholly past the near plane -- and marks its entry; the
+// recomputing raster (k_tile_raster<STAGE, true>, resolve_pixel<DEFER, true>) rebuilds its box, bound,
+// 1/z and steps from its corners (the same operations on the same operands: the same floats).  The
+// clip's slots always keep their records.
+constexpr uint32_t kNoRecBit = 0x80000000u;
+
 // The corner's camera-space and raster position (render.cpp:286, :288).  The two projections share
 // one refined reciprocal of -cv.z where the trimmed division is exact (div_in_range, s3r_common.h);
 // z = (0 * factor) / nz + nz is nz itself unless nz == 0 (0 / 0: the reference's NaN).
@@ -1803,8 +1811,9 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
                                           uint32_t nparts, uint32_t part, uint32_t tiles_x, uint32_t xoff,
                                           RasterRec *__restrict__ recs, uint4 *__restrict__ lv, uint32_t *__restrict__ nlive,
                                           uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin = nullptr,
-                                          uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr) {
+                                          uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr, bool rec = true) {
     uint32_t bx = kDeadBox, by = 0;
+    const bool keep = rec;                              // (norec frames: only the clip's slots keep records)
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
         // the span first (it does not depend on the depth bucket) and the corners stored before the
@@ -1812,23 +1821,25 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
         sp = box_tiles(tile_box(ts.xmin | (ts.xmax << 16), 0u, xoff), ts.ymin | (ts.ymax << 16), band, nparts, part);
         if (sp.n) {
             nt_f4 *q = reinterpret_cast<nt_f4 *>(recs + slot);
-            __builtin_nontemporal_store((nt_f4){ts.rvz[1], ts.rvz[2], dv[0].rv.x, dv[0].rv.y}, q + 1);
-            __builtin_nontemporal_store((nt_f4){dv[1].rv.x, dv[1].rv.y, dv[2].rv.x, dv[2].rv.y}, q + 2);
+            if (keep) {
+                __builtin_nontemporal_store((nt_f4){ts.rvz[1], ts.rvz[2], dv[0].rv.x, dv[0].rv.y}, q + 1);
+                __builtin_nontemporal_store((nt_f4){dv[1].rv.x, dv[1].rv.y, dv[2].rv.x, dv[2].rv.y}, q + 2);
+            }
             const uint32_t zb = f2u(ooz_bound(ts));
             bx = tile_box(ts.xmin | (ts.xmax << 16), zb, xoff);
             by = ts.ymin | (ts.ymax << 16);
             sp.bucket = bx >> 24;
-            __builtin_nontemporal_store((nt_f4){u2f(ts.xmin | (ts.xmax << 16)), u2f(by), u2f(zb), ts.rvz[0]}, q);
+            if (keep) __builtin_nontemporal_store((nt_f4){u2f(ts.xmin | (ts.xmax << 16)), u2f(by), u2f(zb), ts.rvz[0]}, q);
         }
     }
     if (tbin) {
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 16)
         if (bx == 12345u)                               // ablation: no binning
 #endif
-        tile_visit(sp, tiles_x, counts, tbin, slot, 0xFFFFFFFFu, bin_cap, ovf);
+        tile_visit(sp, tiles_x, counts, tbin, rec ? slot : slot | kNoRecBit, 0xFFFFFFFFu, bin_cap, ovf);
         return;
     }
-    wave_append(bx != kDeadBox, make_uint4(bx, by, slot, 0), lv, nlive);
+    wave_append(bx != kDeadBox, make_uint4(bx, by, rec ? slot : slot | kNoRecBit, 0), lv, nlive);
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 1)
     if (bx == 12345u)                                   // ablation: no tile counting
 #endif
@@ -1845,7 +1856,7 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
 // setup is memory-latency-bound).
 // (occupancy caps of 7 / 8 waves per SIMD, 72 / 64 VGPRs, measured slower: 580 -> 605 / 845 us, part 0
 // of 8 129 -> 171 / 218 us; profiles/r05_setup_occ_ab.txt)
-template <bool VS, bool CL>
+template <bool VS, bool CL, bool NOREC>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, const uint32_t *__restrict__ cmap,
                                                     const uint32_t *__restrict__ cperm,
@@ -1916,7 +1927,8 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
-        emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4);
+        emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4,
+                  !NOREC);
     }
 }
 
@@ -2115,12 +2127,37 @@ constexpr uint32_t kDeferPixel = 0xFFFFFFFFu;           // (never a pixel: 0x00R
 // values k_tile_setup computed); a clip-appended or near-plane-crossing winner needs its full setup
 // (slot_setup, the clip) -- with DEFER the pixel returns kDeferPixel for k_tile_resolve_deferred
 // instead (rare, and the clip's registers stay out of the caller).
-template <bool DEFER>
+template <bool DEFER, bool RC = false>
 __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned long long k, uint32_t x, uint32_t y) {
     if (!k) return kBackground;
     const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
     const float ooz = u2f((uint32_t)(k >> 32));
     if (DEFER && s >= sc.ntri) return kDeferPixel;
+    if (RC) {
+        // no record read: the winner set up again from the scene (setup_tri), or its full setup
+        const uint32_t t = s < sc.ntri ? s : s - sc.ntri;
+        Vert d[3];
+        bool near_cut = false;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint32_t ai = sc.aidx[3 * t + c];
+            project_corner(sc.vtx[sc.vidx[3 * t + c]], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[c]);
+            d[c].n = mat_mul(sc.m, sc.nrm[ai]);
+            d[c].pay = sc.pay[ai];
+            near_cut = near_cut || d[c].rv.z < kNear;
+        }
+        TriSetup ts;
+        if (s >= sc.ntri || near_cut) {
+            if (DEFER) return kDeferPixel;
+            slot_setup(s, sc.ntri, sc.vtx, sc.nrm, sc.pay, sc.disc, sc.vidx, sc.aidx, sc.m, sc.factor, sc.sw, sc.sh, ts);
+        } else {
+            setup_tri(d, sc.disc[sc.aidx[3 * t]] != 0, sc.sw, sc.sh, &ts);
+        }
+        const float w0 = short_walk(short_walk(ts.ws[0], ts.dy[0], y - ts.ymin), ts.dx[0], x - ts.xmin);
+        const float w1 = short_walk(short_walk(ts.ws[1], ts.dy[1], y - ts.ymin), ts.dx[1], x - ts.xmin);
+        const float w2 = short_walk(short_walk(ts.ws[2], ts.dy[2], y - ts.ymin), ts.dx[2], x - ts.xmin);
+        return shade(&ts, w0, w1, w2, ooz, sc.tex, sc.ntex);
+    }
     const float4 *q = reinterpret_cast<const float4 *>(sc.recs + s);
     const uint32_t xmin = f2u(q[0].x) & 0xFFFFu, ymin = f2u(q[0].y) & 0xFFFFu;
     float rws[3], rdx[3], rdy[3], rrz[3];
@@ -2165,7 +2202,7 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
 // winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).  (Round 4 measured
 // the split form -- keys through HBM, a per-pixel resolve launch -- slower everywhere: stress scene
 // whole frame 800 -> 854 fps fused, delivered 583 -> 614, part 0 of 8 4 491 -> 4 672; it is gone.)
-template <uint32_t STAGE = kTileStage>
+template <uint32_t STAGE = kTileStage, bool RC = false>
 #ifndef S3R_TOCC
 #define S3R_TOCC 6                     // min waves per SIMD of the fused raster: 80 VGPRs (92 uncapped, occupancy 5);
 #endif                                 // the 256-stage instance stays at 4 (its LDS).  Stress scene, one box
@@ -2251,13 +2288,19 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
                 s_nx = list[base + c + tid];
             }
 #ifdef S3R_BOUNDS
-            if (sc.ntri && s_nx >= 2u * sc.ntri) {
+            if (sc.ntri && (s_nx & ~kNoRecBit) >= 2u * sc.ntri) {
                 printf("S3R_BOUNDS raster: tile %u slot %u >= %u (bins %u)\n", tile, s_nx, 2u * sc.ntri, bin_cap);
                 s_nx = 0;
             }
 #endif
-            const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
-            q0n = q[0]; q1n = q[1]; q2n = q[2];
+            if (RC && (s_nx & kNoRecBit)) {                 // no record: the corners (set up at staging)
+                const uint32_t *vi = sc.vidx + 3ull * (s_nx & ~kNoRecBit);
+                const uint32_t v0 = vi[0], v1 = vi[1], v2 = vi[2];
+                q0n = sc.vtx[v0]; q1n = sc.vtx[v1]; q2n = sc.vtx[v2];
+            } else {
+                const float4 *q = reinterpret_cast<const float4 *>(recs + s_nx);
+                q0n = q[0]; q1n = q[1]; q2n = q[2];
+            }
         }
     };
     fetch(0);
@@ -2302,8 +2345,21 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
         if (tid < STAGE && j < n) {
-            const uint32_t s = s_nx;
-            const float4 q0 = q0n, q1 = q1n, q2 = q2n;
+            const uint32_t s = RC ? s_nx & ~kNoRecBit : s_nx;
+            float4 q0 = q0n, q1 = q1n, q2 = q2n;
+            if (RC && (s_nx & kNoRecBit)) {
+                // the record k_tile_setup would have written, from the corners: box, bound, 1/z, corners
+                Vert d[3];
+                const float4 cc[3] = {q0, q1, q2};
+#pragma unroll
+                for (int k = 0; k < 3; k++) project_corner(cc[k], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[k]);
+                TriSetup ts;
+                raster_part(d, sc.sw, sc.sh, ts);            // (true: the setup binned it)
+                const uint32_t zb = f2u(ooz_bound(ts));
+                q0 = make_float4(u2f(ts.xmin | (ts.xmax << 16)), u2f(ts.ymin | (ts.ymax << 16)), u2f(zb), ts.rvz[0]);
+                q1 = make_float4(ts.rvz[1], ts.rvz[2], d[0].rv.x, d[0].rv.y);
+                q2 = make_float4(d[1].rv.x, d[1].rv.y, d[2].rv.x, d[2].rv.y);
+            }
             const uint32_t bx = f2u(q0.x), by = f2u(q0.y);
             const uint32_t zbits = f2u(q0.z);
             uint32_t lo = 1u, hi = 0u;
@@ -2444,7 +2500,7 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
             const unsigned long long k = in ? ls.key[rr * kKeyStride + cc] : 0ull;
             const uint32_t y = row_of(lr);
             uint32_t v = kBackground;
-            if (in) v = resolve_pixel<true>(sc, k, x, y);
+            if (in) v = resolve_pixel<true, RC>(sc, k, x, y);
             const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
 #ifdef S3R_BOUNDS
             if (in && idx >= (size_t)W * (frame_rows ? (uint32_t)sc.sh : rows_local)) {
@@ -2906,13 +2962,13 @@ template <class K> uint32_t shard_grid(K *kernel, uint64_t work, uint32_t dflt =
     return shard_grid(reinterpret_cast<const void *>(kernel), work, dflt);
 }
 
-template <bool VS, bool CL>
-void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
+template <bool VS, bool CL, bool NOREC>
+void setup_launch_nr(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
                   float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
                   void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
                   hipStream_t st, uint32_t *tbin, uint32_t bin_cap) {
     const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
-    { hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
+    { hipLaunchKernelGGL((k_tile_setup<VS, CL, NOREC>), dim3(shard_grid(k_tile_setup<VS, CL, NOREC>, ntri, CL ? 256 : 1024)), dim3(256),
                        0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, xoff,
                        (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap); after_launch("k_tile_setup", st); }
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
@@ -2920,13 +2976,25 @@ void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const 
                        factor, sw, sh, band, nparts, part, tx, xoff, (RasterRec *)recs, live, clipq, ctr, counts, tbin,
                        bin_cap); after_launch("k_tile_clip", st); }
 }
+template <bool VS, bool CL>
+void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
+                  float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
+                  void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
+                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap, bool norec) {
+    if (norec)
+        setup_launch_nr<VS, CL, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
+                                      ctr, counts, vrv, st, tbin, bin_cap);
+    else
+        setup_launch_nr<VS, CL, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
+                                       ctr, counts, vrv, st, tbin, bin_cap);
+}
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
                        uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag, uint32_t *tbin,
-                       uint32_t bin_cap, uint32_t xoff) {
+                       uint32_t bin_cap, uint32_t xoff, bool norec) {
     const uint64_t ns = tile_slots(W, rows_local, xoff);  // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
@@ -2937,13 +3005,13 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
             { hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
                                cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr); after_launch("k_cluster_cull", st); }
             setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                      ctr, counts, nullptr, st, tbin, bin_cap);
+                                      ctr, counts, nullptr, st, tbin, bin_cap, norec);
         } else if (vrv) {
             setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                      ctr, counts, vrv, st, tbin, bin_cap);
+                                      ctr, counts, vrv, st, tbin, bin_cap, norec);
         } else {
             setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live,
-                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap);
+                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap, norec);
         }
     }
     if (bin_cap) {                                       // bins mode: binned already
@@ -2981,17 +3049,22 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows, uint32_t *counts,
-                                uint32_t bin_cap, uint32_t xoff, uint32_t *sum_host) {
+                                uint32_t bin_cap, uint32_t xoff, uint32_t *sum_host, bool norec) {
     const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
     // frames written into the caller's buffer stage 256 triangles at a time, frames into HBM 128: on
     // the stress scene (one MI355X, profiles/r04_tstage_ab.txt) the wider stage delivers 772 / 726 ->
     // 802 / 803 fps (the raster waits on the link anyway, and half the stage rounds and barriers
-    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy)
+    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy).  The delivered
+    // instance also recomputes the records the setup left out (norec, kNoRecBit)
     const uint32_t capw = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
-    if (frame_rows)
-        { hipLaunchKernelGGL((k_tile_raster<kTileStageLink>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+    if (frame_rows || norec) {
+        if (!frame_rows) {                // (norec frames are delivered ones: render_api.cpp render_tiles)
+            fprintf(stderr, "s3r: a tile frame set up without records needs frame_rows\n");
+            abort();
+        }
+        hipLaunchKernelGGL((k_tile_raster<kTileStageLink, true>), dim3(tx * ty), dim3(kTileThreads), 0, st,
                            (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list,
                            capw, sc, out, 1u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
     else

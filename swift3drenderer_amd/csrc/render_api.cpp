@@ -155,6 +155,7 @@ struct Dev {
     uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
     uint32_t *tile_out = nullptr;
     bool tile_frame_rows = false;
+    bool tile_norec = false;                   // the tile frame's setup writes records for the clip's slots only
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_set = -1;                         // tile path: the last frame's buffer set (refresh_pairs)
@@ -385,7 +386,7 @@ struct Lib {
     uintptr_t unmapped_a = 0;
     uint64_t unmapped_epoch = 0;
     // environment switches read once per library state (release_all resets them: a configure re-reads)
-    int env_row_starts = -1, env_host_uncached = -1, env_slot_cull = -1;
+    int env_row_starts = -1, env_host_uncached = -1, env_slot_cull = -1, env_tile_norec = -1;
     // fill-thread placement: frames in a row whose buffer sat on another node than the placement's
     int fill_node_streak = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
@@ -998,7 +999,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
                                list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff,
-                               d.tile_sum_dev + kSumWords * p);
+                               d.tile_sum_dev + kSumWords * p, d.tile_norec);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());
@@ -1168,7 +1169,7 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
                           d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p],
                           d.tile_cursor[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl,
                           d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u,
-                          d.tile_xoff);
+                          d.tile_xoff, d.tile_norec);
         wait_tile_summary(d, p, geo);
         if (!bins) {
             grow_tile_list(d, p, sum[2]);
@@ -1243,10 +1244,18 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (bins_on(d)) ensure_bins(d, nt);
     const bool bins = bins_on(d);
     if (!bins) ensure_live(d);
+    // frames into the caller's buffer: no raster records for the slots the raster can set up again
+    // (kernels.hip kNoRecBit; their fragment stage is the recomputing raster).  Stress scene, one
+    // MI355X: setup 545 -> 425 us, its traffic 1.34 -> 0.84 GB, delivered frames 831-833 -> 928-930 fps.
+    // Frames into HBM keep the records: there the raster's recomputation (at occupancy 5: 80 VGPRs
+    // spill) costs more than the setup saves -- whole frame 1 105 -> 1 012 fps, part 0 of 8 at the
+    // library's 135-row band 6 677 -> 6 370 (profiles/r05_rec0_ab.txt).  S3R_TILE_NOREC=0: records for
+    // every frame.
+    d.tile_norec = frame_rows && env_on(g.env_tile_norec, "S3R_TILE_NOREC");
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff);
+                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff, d.tile_norec);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are

@@ -48,6 +48,14 @@
 #   clshallow frame parts' setup (clusters) one deep again (product) vs two deep (prev build)
 #   linfast   k_fragment: triangles whose three components are exactly linear over the chunk skip the
 #             table fill (values c + k delta where read; linf build, S3R_LINFAST) vs every chunk tabled
+#   (rec0     every tile frame without records -- an S3R_REC0 build since folded into the product for
+#             delivered frames; its numbers and counters are in r05_rec0_ab.txt, the recipe is gone)
+#   norec     delivered tile frames without raster records for the slots the raster sets up again
+#             (product) vs the build before (prev) and S3R_TILE_NOREC=0: GPU suite, stress N=1 / part 0 of 8,
+#             bench lines, delivered-frame rocprof                   -> r05_rec0_ab.txt
+#   (norec2   frame parts without records too (a build of that session, S3R_TILE_NOREC=1 then) vs delivered
+#             frames only (=2, now the product): not kept -- part 0 of 8 at the library's 135-row band
+#             6 677 -> 6 370 fps (+7 % at 16-row bands); r05_rec0_ab.txt, the recipe is gone)
 #   slotcull  k_geometry launching only the slots the host's cull keeps (product) vs every slot
 #             (S3R_SLOT_CULL=0): parity suites, 4K / P_id / 8K / 1080p bench lines, geometry timelines
 #   slotcull2 the same, device and delivered rates only, three alternating repetitions, overhead probes
@@ -314,6 +322,25 @@ slotcull3)
   done
   for rep in 1 2; do
     BENCH_EXTRA='--scene full --width 1920 --height 1080' bash tools/lib_ab.sh 'nocull full1080||S3R_SLOT_CULL=0' 'cull full1080||' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done ;;
+norec)
+  gpu_suite $OUT/gputest.log tests || exit 1
+  stress_data || exit 1
+  NS="1 8" PROF=1 PROF_NS="1 8" bash tools/stress_lib_ab.sh 'norec||' 'prev|build/librender_prev.so|' 2>&1 | tee $OUT/ab.txt || exit 1
+  for rep in 1 2; do
+    BENCH_EXTRA="--scene icosa-stress --pose P_id --data $D" bash tools/lib_ab.sh 'norec stress||' 'prev stress|build/librender_prev.so|' \
+        'rec stress||S3R_TILE_NOREC=0' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  done
+  bash tools/lib_ab.sh 'norec 4K||' 'prev 4K|build/librender_prev.so|' 2>&1 | tee -a $OUT/ab.txt || exit 1
+  for spec in 'norec|' 'prev|build/librender_prev.so'; do
+    IFS='|' read -r tag lib <<< "$spec"
+    env ${lib:+S3R_LIB=$lib} timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/del_$tag -o run -- \
+        python3 bench.py --scene icosa-stress --pose P_id --data $D --steps 60 --warmup 10 --no-cpu-baseline --no-device > $OUT/del_$tag.log 2>&1 || exit 1
+    f=$(find $OUT/del_$tag -name '*kernel_stats.csv' | head -1)
+    echo "== $tag delivered (rocprof)"; python3 -c "
+import csv
+for r in list(csv.DictReader(open('$f')))[:6]: print('  %-60s %8s calls  avg %9.1f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))" | tee -a $OUT/ab.txt
+    find $OUT/del_$tag -name '*kernel_trace.csv' -delete
   done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
