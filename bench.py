@@ -627,9 +627,13 @@ def run_rank0(a, N, np, torch):
         'setup_ms': round(geo_ms / max(nfr, 1), 5),
         'setup_bytes_per_frame': (16 * nv + 4 * ni + 4 * pairs) if path == 2 else None,
         'setup_traffic': load_traffic(workload, 'setup_hbm_bytes_per_launch') if path == 2 else None,
+        # delivered tile frames write no record for the slots the raster rebuilds (Delivered
+        # tile frames without records): their setup's PMC bytes per frame
+        'setup_traffic_delivered': load_traffic(workload, 'delivered_setup_hbm_bytes_per_launch') if path == 2 else None,
         'setup_bytes_note': ('tile path, a lower bound: vertices 16 B and indices 4 B read, a 4-B bin entry '
-                             'written per binned entry; the 64-B raster record of each live slot is not counted '
-                             '(bins mode does not count live slots)') if path == 2 else None,
+                             'written per binned entry; the 48-B raster record of each live slot is not counted '
+                             '(bins mode does not count live slots); setup_traffic: device-resident frames, '
+                             'setup_traffic_delivered: delivered frames (PMC)') if path == 2 else None,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
                      'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,

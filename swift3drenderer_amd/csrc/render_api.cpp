@@ -339,6 +339,8 @@ struct Lib {
     std::vector<uint8_t> near_side;
     bool clip_slots = true;                    // this frame: launch k_geometry's clip-appended slots
     SlotMask live{};                           // this frame: the slots k_geometry launches (cull_slots)
+    // the camera state clip_slots and live were computed for (frame_begin: unchanged -> reused)
+    struct CullKey { Mat34 m; float factor; uint32_t W, H; bool valid; } cull_key{};
     std::vector<double> near_rv;               // per vertex: screen x, y and their error bound (cull_slots)
     bool clusters = true;                      // tile path: cull clusters before the setup (S3R_CLUSTERS)
     bool clusters_whole = false;               // ... also for whole frames (S3R_CLUSTERS=2)
@@ -537,6 +539,7 @@ HostScene read_scene() {
     g.nv = (uint32_t)nv; g.na = (uint32_t)na; g.ntri = (uint32_t)ntri; g.ntex = (uint32_t)nt;
     g.nindices = ni;
     g.near_vtx.clear(); g.near_vidx.clear();
+    g.cull_key.valid = false;
     if (ntri <= kNearCheckMaxTri && 2 * ntri <= kRowPathMaxSlots) { g.near_vtx = s.vtx; g.near_vidx = s.vidx; }
     // clusters for the tile path's per-frame cull (scenes the tile path renders by default, or any
     // scene with S3R_CLUSTERS=2): connected meshes of 8-32 triangles, larger ones cut, smaller pooled
@@ -761,9 +764,14 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
         g.factor = kNear * (float)height / (2 * config_scale());          // render.cpp:279
         unregister_all();
     }
+    // the near-plane check and the slot cull depend on the camera matrix, factor and frame size only
+    // (and the scene, whose load invalidates the key): a frame that repeats them reuses their result
+    Lib::CullKey &k = g.cull_key;
+    if (k.valid && k.factor == g.factor && k.W == width && k.H == height && !memcmp(&k.m, &g.m, sizeof(Mat34))) return;
     g.clip_slots = near_plane_crossing();
     g.live.on = 0;
     if (!g.clip_slots && env_on(g.env_slot_cull, "S3R_SLOT_CULL")) cull_slots(width, height);
+    k = Lib::CullKey{g.m, g.factor, width, height, true};
 }
 
 TimingSlot *timing_slot(Dev &d) {

@@ -60,6 +60,7 @@
 #             (S3R_SLOT_CULL=0): parity suites, 4K / P_id / 8K / 1080p bench lines, geometry timelines
 #   slotcull2 the same, device and delivered rates only, three alternating repetitions, overhead probes
 #   slotcull3 1080p delivered frames, the variants in the other order
+#   cullparts part 0 of 8 and whole 4K frames (overhead probes, host enqueue time), cull vs no cull
 #                                                                   -> r05_slot_cull_ab.txt
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
@@ -341,6 +342,15 @@ norec)
 import csv
 for r in list(csv.DictReader(open('$f')))[:6]: print('  %-60s %8s calls  avg %9.1f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))" | tee -a $OUT/ab.txt
     find $OUT/del_$tag -name '*kernel_trace.csv' -delete
+  done ;;
+cullparts)
+  gpu_suite $OUT/parity.log tests/test_gpu_parity.py tests/test_host_loop.py tests/test_multi_device.py tests/test_multi.py || exit 1
+  for rep in 1 2 3; do
+    for spec in "cull|" "nocull|S3R_SLOT_CULL=0"; do
+      IFS='|' read -r tag envs <<< "$spec"
+      probe "$tag N8" $envs -- --nparts 8 --steps 3000 | tee -a $OUT/probe.txt || exit 1
+      probe "$tag N1" $envs -- --steps 2000 | tee -a $OUT/probe.txt || exit 1
+    done
   done ;;
 *)
   echo "unknown recipe $R"; exit 2 ;;
