@@ -1856,6 +1856,9 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
 // setup is memory-latency-bound).
 // (occupancy caps of 7 / 8 waves per SIMD, 72 / 64 VGPRs, measured slower: 580 -> 605 / 845 us, part 0
 // of 8 129 -> 171 / 218 us; profiles/r05_setup_occ_ab.txt)
+// (the record-writing instances take 85-87 VGPRs, occupancy 5, since the NOREC ones joined them;
+// capped at 80 -- occupancy 6, 12-20 B spilled -- the pipelined stress frame lost 3 %, part 0 of 8
+// 6 %: profiles/r05_rec0_ab.txt)
 template <bool VS, bool CL, bool NOREC>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, const uint32_t *__restrict__ cmap,

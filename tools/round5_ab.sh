@@ -60,6 +60,8 @@
 #             (S3R_SLOT_CULL=0): parity suites, 4K / P_id / 8K / 1080p bench lines, geometry timelines
 #   slotcull2 the same, device and delivered rates only, three alternating repetitions, overhead probes
 #   slotcull3 1080p delivered frames, the variants in the other order
+#   (socc6    the record-writing k_tile_setup instances capped at 80 VGPRs: negative, in r05_rec0_ab.txt;
+#             the recipe and its S3R_SOCC_REC build are gone)
 #   cullparts part 0 of 8 and whole 4K frames (overhead probes, host enqueue time), cull vs no cull
 #                                                                   -> r05_slot_cull_ab.txt
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
