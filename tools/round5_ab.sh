@@ -51,7 +51,8 @@
 #   (rec0     every tile frame without records -- an S3R_REC0 build since folded into the product for
 #             delivered frames; its numbers and counters are in r05_rec0_ab.txt, the recipe is gone)
 #   norec     delivered tile frames without raster records for the slots the raster sets up again
-#             (product) vs the build before (prev) and S3R_TILE_NOREC=0: GPU suite, stress N=1 / part 0 of 8,
+#             (product) vs the build before (prev: build_variant("prev") from commit 64b5d0e~3) and
+#             S3R_TILE_NOREC=0: GPU suite, stress N=1 / part 0 of 8,
 #             bench lines, delivered-frame rocprof                   -> r05_rec0_ab.txt
 #   (norec2   frame parts without records too (a build of that session, S3R_TILE_NOREC=1 then) vs delivered
 #             frames only (=2, now the product): not kept -- part 0 of 8 at the library's 135-row band
