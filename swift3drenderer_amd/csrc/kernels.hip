@@ -2137,28 +2137,40 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
     const float ooz = u2f((uint32_t)(k >> 32));
     if (DEFER && s >= sc.ntri) return kDeferPixel;
     if (RC) {
-        // no record read: the winner set up again from the scene (setup_tri), or its full setup
+        // no record read: the winner set up again from the scene -- its positions first (raster part,
+        // the walk to the pixel), then its shading constants -- or its full setup (clip)
         const uint32_t t = s < sc.ntri ? s : s - sc.ntri;
-        Vert d[3];
-        bool near_cut = false;
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const uint32_t ai = sc.aidx[3 * t + c];
-            project_corner(sc.vtx[sc.vidx[3 * t + c]], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[c]);
-            d[c].n = mat_mul(sc.m, sc.nrm[ai]);
-            d[c].pay = sc.pay[ai];
-            near_cut = near_cut || d[c].rv.z < kNear;
-        }
         TriSetup ts;
-        if (s >= sc.ntri || near_cut) {
-            if (DEFER) return kDeferPixel;
-            slot_setup(s, sc.ntri, sc.vtx, sc.nrm, sc.pay, sc.disc, sc.vidx, sc.aidx, sc.m, sc.factor, sc.sw, sc.sh, ts);
-        } else {
-            setup_tri(d, sc.disc[sc.aidx[3 * t]] != 0, sc.sw, sc.sh, &ts);
+        float w0, w1, w2;
+        bool near_cut = false;
+        {
+            Vert d[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                project_corner(sc.vtx[sc.vidx[3 * t + c]], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[c]);
+                near_cut = near_cut || d[c].rv.z < kNear;
+            }
+            if (s >= sc.ntri || near_cut) {
+                if (DEFER) return kDeferPixel;
+                slot_setup(s, sc.ntri, sc.vtx, sc.nrm, sc.pay, sc.disc, sc.vidx, sc.aidx, sc.m, sc.factor, sc.sw, sc.sh, ts);
+            } else {
+                raster_part(d, sc.sw, sc.sh, ts);
+            }
+            w0 = short_walk(short_walk(ts.ws[0], ts.dy[0], y - ts.ymin), ts.dx[0], x - ts.xmin);
+            w1 = short_walk(short_walk(ts.ws[1], ts.dy[1], y - ts.ymin), ts.dx[1], x - ts.xmin);
+            w2 = short_walk(short_walk(ts.ws[2], ts.dy[2], y - ts.ymin), ts.dx[2], x - ts.xmin);
         }
-        const float w0 = short_walk(short_walk(ts.ws[0], ts.dy[0], y - ts.ymin), ts.dx[0], x - ts.xmin);
-        const float w1 = short_walk(short_walk(ts.ws[1], ts.dy[1], y - ts.ymin), ts.dx[1], x - ts.xmin);
-        const float w2 = short_walk(short_walk(ts.ws[2], ts.dy[2], y - ts.ymin), ts.dx[2], x - ts.xmin);
+        if (s < sc.ntri && !near_cut) {
+            Vert d[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const uint32_t ai = sc.aidx[3 * t + c];
+                d[c].cv = mat_mul(sc.m, sc.vtx[sc.vidx[3 * t + c]]);              // (as project_corner: :286)
+                d[c].n = mat_mul(sc.m, sc.nrm[ai]);
+                d[c].pay = sc.pay[ai];
+            }
+            shading_part(d, sc.disc[sc.aidx[3 * t]] != 0, ts);
+        }
         return shade(&ts, w0, w1, w2, ooz, sc.tex, sc.ntex);
     }
     const float4 *q = reinterpret_cast<const float4 *>(sc.recs + s);
@@ -2269,10 +2281,17 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
     }
     // software pipeline: stage c0 + STAGE's list entries and records are loaded into registers
     // while stage c0's items run
-    uint32_t s_nx = 0;
+    uint32_t s_nx = 0, b_nx = 0;                 // (b_nx: the entry's depth bucket, RC)
     float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n;
     auto fetch = [&](uint32_t c) {
         if (tid < STAGE && c + tid < n) {
+            if (RC) {                                    // the entry's depth bucket (its bound's ceiling)
+                uint32_t bb = 0;
+#pragma unroll
+                for (uint32_t step = 16; step >= 1u; step >>= 1)
+                    if (ls.bstart[bb + step] <= c + tid) bb += step;
+                b_nx = bb;
+            }
             if (bin_cap) {
                 const uint32_t v = c + tid;
                 uint32_t b = 0;                                  // the bucket holding entry v
@@ -2358,7 +2377,10 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
                 for (int k = 0; k < 3; k++) project_corner(cc[k], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[k]);
                 TriSetup ts;
                 raster_part(d, sc.sw, sc.sh, ts);            // (true: the setup binned it)
-                const uint32_t zb = f2u(ooz_bound(ts));
+                // the setup's bound (ooz_bound) lies below its depth bucket's ceiling: that ceiling serves as
+                // the row cull's bound (coarser, never below the true one; bucket 0: none, never culled) --
+                // ooz_bound here cost 80-VGPR spills (36 -> 8 B/lane): stress raster 510 -> 498 us
+                const uint32_t zb = bucket_ceiling(b_nx) - 1u;
                 q0 = make_float4(u2f(ts.xmin | (ts.xmax << 16)), u2f(ts.ymin | (ts.ymax << 16)), u2f(zb), ts.rvz[0]);
                 q1 = make_float4(ts.rvz[1], ts.rvz[2], d[0].rv.x, d[0].rv.y);
                 q2 = make_float4(d[1].rv.x, d[1].rv.y, d[2].rv.x, d[2].rv.y);
@@ -3059,14 +3081,14 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
     // frames written into the caller's buffer stage 256 triangles at a time, frames into HBM 128: on
     // the stress scene (one MI355X, profiles/r04_tstage_ab.txt) the wider stage delivers 772 / 726 ->
     // 802 / 803 fps (the raster waits on the link anyway, and half the stage rounds and barriers
-    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy).  The delivered
-    // instance also recomputes the records the setup left out (norec, kNoRecBit)
+    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy).  norec frames take
+    // the recomputing instances (the records the setup left out rebuilt at staging, kNoRecBit)
     const uint32_t capw = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
-    if (frame_rows || norec) {
-        if (!frame_rows) {                // (norec frames are delivered ones: render_api.cpp render_tiles)
-            fprintf(stderr, "s3r: a tile frame set up without records needs frame_rows\n");
-            abort();
-        }
+    if (!frame_rows && norec)
+        { hipLaunchKernelGGL((k_tile_raster<kTileStage, true>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+                           (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list, capw, sc,
+                           out, 0u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
+    else if (frame_rows) {
         hipLaunchKernelGGL((k_tile_raster<kTileStageLink, true>), dim3(tx * ty), dim3(kTileThreads), 0, st,
                            (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list,
                            capw, sc, out, 1u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }

@@ -1252,14 +1252,17 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (bins_on(d)) ensure_bins(d, nt);
     const bool bins = bins_on(d);
     if (!bins) ensure_live(d);
-    // frames into the caller's buffer: no raster records for the slots the raster can set up again
-    // (kernels.hip kNoRecBit; their fragment stage is the recomputing raster).  Stress scene, one
-    // MI355X: setup 545 -> 425 us, its traffic 1.34 -> 0.84 GB, delivered frames 831-833 -> 928-930 fps.
-    // Frames into HBM keep the records: there the raster's recomputation (at occupancy 5: 80 VGPRs
-    // spill) costs more than the setup saves -- whole frame 1 105 -> 1 012 fps, part 0 of 8 at the
-    // library's 135-row band 6 677 -> 6 370 (profiles/r05_rec0_ab.txt).  S3R_TILE_NOREC=0: records for
-    // every frame.
-    d.tile_norec = frame_rows && env_on(g.env_tile_norec, "S3R_TILE_NOREC");
+    // no raster records for the slots the raster can set up again (kernels.hip kNoRecBit; the
+    // fragment stage is then the recomputing raster).  Stress scene, one MI355X
+    // (profiles/r05_rec0_ab.txt): setup 548-554 -> 434 us, its traffic 1.34 -> 0.84 GB; delivered
+    // frames 831-833 -> 915-924 fps; frames into HBM (the raster 423 -> 498 us) 1 151 -> 1 174 fps
+    // whole, part 0 of 8 at the 135-row band 6 503-6 524 -> 6 846-6 880.  S3R_TILE_NOREC=0: records for
+    // every frame, 2: for frames into HBM only.
+    if (g.env_tile_norec < 0) {
+        const char *e = getenv("S3R_TILE_NOREC");
+        g.env_tile_norec = e ? atoi(e) : 1;
+    }
+    d.tile_norec = g.env_tile_norec == 1 || (frame_rows && g.env_tile_norec == 2);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,

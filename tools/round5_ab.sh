@@ -63,6 +63,10 @@
 #   slotcull3 1080p delivered frames, the variants in the other order
 #   (socc6    the record-writing k_tile_setup instances capped at 80 VGPRs: negative, in r05_rec0_ab.txt;
 #             the recipe and its S3R_SOCC_REC build are gone)
+#   rcres     the recomputing raster's resolve in two phases (positions, then shading constants: 36 B
+#             spilled at 80 VGPRs instead of 128) for every frame (S3R_TILE_NOREC=2 of that build) vs
+#             records, and with the depth bucket's ceiling as the staged bound (rcbb build: 8 B) -- the
+#             product since; the recipe's builds and knob values are gone  -> r05_rec0_ab.txt
 #   cullparts part 0 of 8 and whole 4K frames (overhead probes, host enqueue time), cull vs no cull
 #                                                                   -> r05_slot_cull_ab.txt
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
