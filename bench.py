@@ -46,7 +46,8 @@ METRIC = 'frames/sec + Mpixels/s at 3840x2160, data.bin scene; 1/2/4/8-GPU scali
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md, HBM3E peak (spec)
 LINK_PEAK_GBS = 63.0     # MI355X_MICROARCH.md, host link PCIe Gen5 x16 per direction (spec)
 TRI_SETUP_BYTES = 240    # sizeof(TriSetup)
-RASTER_REC_BYTES = 64    # sizeof(RasterRec), tile path
+ENTRY_SOURCE_BYTES = 12 + 3 * 16   # tile path, per binned entry: the 3 vertex indices and 3 corners the
+                                    # raster rebuilds its record from (Tile frames without records)
 MIN_TIMED = 200          # >= 200 frames after 20 warm-up frames
 MIN_WARMUP = 20
 
@@ -516,8 +517,9 @@ def run_rank0(a, N, np, torch):
         if path == 2:
             # tile path, fragment stage = k_tile_raster<true> (raster and shading fused) + the short
             # k_tile_resolve_deferred: the framebuffer rows, and per binned (slot, tile) entry its 4-B bin
-            # entry and 64-B raster record read (pairs: the frame's binned entries, s3r_scene_counts)
-            return 'k_tile_raster<true> (fused) + k_tile_resolve_deferred', 4 * W * rows + (4 + RASTER_REC_BYTES) * pairs
+            # entry and the indices and corners its record is rebuilt from (pairs: the frame's binned
+            # entries, s3r_scene_counts)
+            return 'k_tile_raster (fused) + k_tile_resolve_deferred', 4 * W * rows + (4 + ENTRY_SOURCE_BYTES) * pairs
         # row path, k_fragment: the framebuffer rows + the ripmap texels it may sample + the triangle
         # setup records it reads
         return 'k_fragment', 4 * W * rows + 4 * ntex + TRI_SETUP_BYTES * nslots
