@@ -271,6 +271,34 @@ def test_tile_bands_reassemble(gpu_renderer, icosa_dir, band, nparts):
     assert np.array_equal(got, full), diff(got, full)
 
 
+@pytest.mark.parametrize('norec', ['0', '1', '2'])
+def test_record_modes_match_oracle(gpu_renderer, icosa_dir, scene_dir, monkeypatch, norec):
+    """The tile setup's raster records: none for the slots the raster rebuilds (S3R_TILE_NOREC=1, the
+    default: kernels.hip kNoRecBit, the recomputing raster and resolve), records for every slot (0), or
+    for frames into HBM only (2) -- delivered frames and a device-resident whole frame, on the stress
+    scene and on the packaged scene crossing the near plane (clip slots keep their records in every
+    mode), each against the oracle."""
+    import torch
+    monkeypatch.setenv('S3R_TILE_NOREC', norec)
+    r = gpu_renderer
+    for path, pose, (w, h) in [(icosa_dir[2000], 'P_id', (1280, 720)), (scene_dir['full'], 'P_clip', (640, 480))]:
+        r.configure(path)                              # (the library re-reads its environment)
+        r.set_raster_path('tiles')
+        try:
+            script = poses.script(pose)
+            want = oracle_render_pose(path, script, w, h, extra_frames=1)
+            got = render_pose(r, path, script, w, h, extra_frames=1)
+            assert np.array_equal(got, want), f'{pose} delivered: ' + diff(got, want)
+            buf = torch.empty((h, w), dtype=torch.int32, device='cuda')
+            hold = (0, 0, 0, 0) + tuple(script[-1][4:6])
+            r.render_bands(hold, w, h, h, 1, 0, buf.data_ptr(), 0)
+            torch.cuda.synchronize()
+            dev = buf.cpu().numpy().view(np.uint32)
+            assert np.array_equal(dev, want), f'{pose} in HBM: ' + diff(dev, want)
+        finally:
+            r.set_raster_path('auto')
+
+
 def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
     """Row path and tile path give the same 4K frame (both are exact)."""
     path = scene_dir['full']
