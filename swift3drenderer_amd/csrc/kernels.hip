@@ -320,7 +320,11 @@ constexpr uint32_t kTPB = 21;          // triangles per batch: lane = 3 * t + co
 constexpr uint32_t kWaves = S3R_WAVES; // one wave per row: a workgroup is kWaves consecutive local rows
 static_assert(kWaves == 4, "pair records carry the walk state of 4 rows (s3r_kernels.h)");
 static_assert(kWaves * 6 <= 32, "host fill: a bin's chunk mask (rows x chunks) fits 32 bits");
-constexpr uint32_t kListMax = 128;     // triangles listed per workgroup (rows x segment)
+// triangles listed per workgroup (rows x segment) by the in-kernel list rounds of bins met by more than
+// kPairMax triangles: five batches.  (128 until round 5; with the padded tables, kTabStride, a workgroup's
+// LDS must stay within 26 KiB -- 6 workgroups per CU at the LDS's allocation granularity: at 27 248 B the
+// launch ran 5 per CU and the 4K kernel took 52.0 instead of 48.7 us, profiles/r06_tabpad_ab.txt.)
+constexpr uint32_t kListMax = 5 * kTPB;
 #ifndef S3R_STATE_BATCHES
 #define S3R_STATE_BATCHES 4
 #endif
@@ -347,6 +351,15 @@ constexpr uint32_t kPX = S3R_PX;       // pixels per lane: a chunk is 64 * kPX c
 constexpr uint32_t kChunk = 64u * kPX;
 constexpr uint32_t kStateBatches = S3R_STATE_BATCHES;  // batches whose walk state persists in LDS
 constexpr uint32_t kTables = S3R_TABLES;  // per wave: 64-entry exact-value tables, non-linear chunks
+#ifndef S3R_TAB_PAD
+#define S3R_TAB_PAD 4                  // floats of padding per table row (see kTabStride)
+#endif
+// A table row is kChunk floats plus S3R_TAB_PAD: the fill's ds_write_b128 of up to kTables lanes at
+// the same column lands, in each 8-lane group, on eight different 4-bank groups (row stride 68 words
+// = 4 banks mod 32) instead of the same four banks (stride 64 words: an 8-way conflict, 35 % of the
+// launch's LDS cycles in round 5).  The pixel reads stay lane-contiguous.
+constexpr uint32_t kTabStride = kChunk + S3R_TAB_PAD;
+static_assert(kTabStride % 4u == 0u, "16-B aligned table rows");
 
 struct alignas(16) Entry {              // 48 B per listed triangle (LDS, shared by the 4 waves)
     uint32_t slot, xmin, xmax, ymin;
@@ -360,13 +373,14 @@ struct FragShared {
     Entry ent[kListMax];
     float st_c[kWaves][kStateBatches * 64];
     uint32_t st_k[kWaves][kStateBatches * 64];
-    float4 tab4[kWaves][kTables][kChunk / 4];  // exact S(c, d, k), k < kChunk, filled by sequential adds
+    float4 tab4[kWaves][kTables][kTabStride / 4];  // exact S(c, d, k), k < kChunk, filled by sequential adds
     uint32_t cnt, next;
     uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
     uint32_t bgm[kWaves];                // host fill: per wave (row), its chunks left to the host
     uint32_t wwork[kWaves];              // per wave: its work units (the bin's cost, order_bins)
 };
 static_assert(offsetof(FragShared, tab4) % 16 == 0, "16-B table rows");
+static_assert(sizeof(FragShared) <= 26u * 1024u, "k_fragment: 6 workgroups per CU (see kListMax)");
 // k_fragment stages a bin's pair records in tab4 before the chunk loop (s3r_kernels.h kPairMax x
 // kPairWords uint4): a tuning build with fewer tables must still leave room for them.
 static_assert(sizeof(((FragShared *)nullptr)->tab4) >= 64u * 8u * sizeof(uint4),
@@ -555,20 +569,44 @@ __device__ void order_bins(const uint32_t *__restrict__ cost, uint32_t n, uint32
 constexpr uint32_t kGeoCntStride = 16;           // uint32 words: one 64-B line per row block
 constexpr uint32_t kGeoCntMax = 256;             // row blocks with a counter (more: k_sky_flags)
 static_assert(kGeoCntMax * kGeoCntStride == kGeoCounterWords, "geometry counters: s3r_kernels.h's size");
+// The publisher's spin is bounded: past spin_ticks of the device clock (100 MHz) it stores
+// {kDiagPublisherTimeout, rb, arrivals seen, arrivals} into err (host-coherent) and returns without
+// publishing; the host's fill threads report it and end the process (render_api.cpp fill_worker).
 struct SkyFlags {
     uint32_t *flags;                  // null: no host fill
     uint32_t *probe;
     uint32_t *geo_cnt;
     uint32_t tag, gpu_eighths;
+    uint32_t *err;
+    uint32_t arrivals;                // geometry workgroups per row block (the host's launch count)
+    uint32_t spin_ticks;
 };
 
 // the row block rb's bins: [rb * rb_bins, (rb + 1) * rb_bins), rb_bins = its fragment row blocks x segs
 __device__ void publish_sky_flags(const SkyFlags &sf, const uint32_t *__restrict__ bincnt, uint32_t nbins,
-                                  uint32_t rb_bins, uint32_t rb, uint32_t arrivals) {
+                                  uint32_t rb_bins, uint32_t rb) {
     uint32_t *cnt = sf.geo_cnt + rb * kGeoCntStride;
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < arrivals) __builtin_amdgcn_s_sleep(2);
+    __shared__ uint32_t timed_out;
+    if (threadIdx.x == 0) {
+        timed_out = 0u;
+        const uint64_t t0 = wall_clock64();
+        uint32_t seen;
+        while ((seen = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < sf.arrivals) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > sf.spin_ticks) {
+                timed_out = 1u;
+                if (sf.err) {
+                    __hip_atomic_store(sf.err + 1, rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(sf.err + 2, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(sf.err + 3, sf.arrivals, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(sf.err, kDiagPublisherTimeout, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                break;
+            }
+        }
+    }
     __syncthreads();
+    if (timed_out) return;
     const uint32_t b0 = rb * rb_bins, b1 = min(nbins, b0 + rb_bins);
     // kPubUnroll counts per thread in flight at once (the loads go to memory: one round trip each)
     constexpr uint32_t kPubUnroll = 4;
@@ -662,7 +700,7 @@ __global__ void __launch_bounds__(3 * kGeoRows, S3R_GEO_OCC) k_geometry(
     // publishers, the dead-slot marker (host cull), geometry
     const uint32_t pub0 = order ? 1u : 0u, mark0 = pub0 + (sky.flags ? nrb : 0u), first = mark0 + live.on;
     if (sky.flags && g0 < mark0) {
-        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0, live.on ? live.nlive : nslots);
+        publish_sky_flags(sky, bincnt, nbins, (kGeoRows / kWaves) * segs, g0 - pub0);
         return;
     }
     if (live.on && g0 == mark0) {
@@ -972,7 +1010,7 @@ constexpr uint32_t kWorkFill = 12, kWorkTest = 4, kWorkTexture = 32, kWorkColour
 // of the next chunk.  Tables hold kTables components = kTables / 3 triangles: a chunk met by more runs
 // in groups, in list (slot) order -- the reference's order, which decides depth ties.
 static_assert(kPX == 1u && kTables % 3u == 0u, "one pixel per lane, whole triangles per table group");
-__device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane, float (*tab)[kChunk], uint32_t xl,
+__device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane, float (*tab)[kTabStride], uint32_t xl,
                                              float (&depth)[kPX], int (&win)[kPX], float (&bw0)[kPX],
                                              float (&bw1)[kPX], float (&bw2)[kPX], float &last, uint32_t &wk) {
     last = v.c;
@@ -1237,7 +1275,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                                     : (v.k0 == r0_sk + 1u ? r0_sc + v.d : walk(r0_sc, v.d, v.k0 - r0_sk S3R_IT(p_chunk)));
             }
             float last;
-            alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
+            alltab_chunk(v, lane, reinterpret_cast<float (*)[kTabStride]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
             if (v.ov) { r0_sc = last; r0_sk = v.k0 + v.m - 1u; }
 #ifdef S3R_STATS
             st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
@@ -1281,7 +1319,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
                     }
                 }
                 float last;
-                alltab_chunk(v, lane, reinterpret_cast<float (*)[kChunk]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
+                alltab_chunk(v, lane, reinterpret_cast<float (*)[kTabStride]>(sh.tab4[wave]), x, depth, win, bw0, bw1, bw2, last, wk);
                 if (v.ov && stateful) { st_c[b * 64 + lane] = last; st_k[b * 64 + lane] = v.k0 + v.m - 1u; }
 #ifdef S3R_STATS
                 st_batches += __ballot(v.ov) != 0ull ? 1u : 0u;
@@ -2701,6 +2739,27 @@ void stats_read(unsigned long long out[24], bool reset) {
 #endif
 }
 
+// ------------------------------------------------------------------ bounded-wait test hook
+// One wave that spins `ticks` of the 100 MHz device clock and exits: a stage that is late but always
+// finishes (S3R_TEST_HOLD_MS, render_api.cpp; tests/test_stall.py).
+__global__ void __launch_bounds__(64) k_test_hold(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+void launch_test_hold(uint32_t ms, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_hold, dim3(1), dim3(64), 0, st, (uint64_t)ms * 100000ull);
+}
+
+uint32_t device_spin_ticks() {
+    static const uint32_t ticks = [] {
+        const char *e = getenv("S3R_SPIN_MS");
+        const long ms = e ? atol(e) : 0;
+        return (uint32_t)(ms > 0 && ms < 40000 ? ms : 2000) * 100000u;
+    }();
+    return ticks;
+}
+
 // ------------------------------------------------------------------ launchers
 // S3R_CHECK=1: each launch synchronised and checked (s3r_kernels.h).  The context is per host
 // thread: with several devices behind updateAndRender each device's worker launches its own part.
@@ -2722,7 +2781,10 @@ void check_context(int device, uint32_t frame, const char *stage) {
 void after_launch(const char *kernel, hipStream_t st) {
     if (!check_launches()) return;
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) {
+        sync_stream_bounded(st, t_check_stage, kernel, t_check_dev, t_check_frame);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess) {
         fprintf(stderr, "s3r: S3R_CHECK: %s after %s (device %d, frame %u, %s)\n", hipGetErrorName(e), kernel,
                 t_check_dev, t_check_frame, t_check_stage);
@@ -2804,7 +2866,7 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
                                   st, nullptr, nullptr, 0, vtx, nrm, pay, disc, vidx, aidx, ntri, m, factor, W, H, band,
                                   nparts, part, rows_local, segs, kChunk * g_segch, tris, rowtab, bincnt, pairs,
                                   (uint32_t)fragment_bins(W, rows_local), order, nrb,
-                                  SkyFlags{nullptr, nullptr, nullptr, 0u, 0u}, row_starts ? 1u : 0u, nslots, lm); after_launch("k_geometry", st); }
+                                  SkyFlags{}, row_starts ? 1u : 0u, nslots, lm); after_launch("k_geometry", st); }
         }
         if (gsf)
             launch_sky_flags(bincnt, fragment_bins(W, rows_local), gsf->flags, gsf->tag, gsf->probe, gsf->gpu_eighths,
@@ -2813,8 +2875,20 @@ void launch_geometry(const float4 *vtx, const float4 *nrm, const float4 *pay, co
             (void)hipEventRecord(done, st);
         return;
     }
-    const SkyFlags sky = gsf ? SkyFlags{gsf->flags, gsf->probe, gsf->geo_cnt, gsf->tag, gsf->gpu_eighths}
-                             : SkyFlags{nullptr, nullptr, nullptr, 0u, 0u};
+    // the publishers wait for one arrival per geometry workgroup of their row block: per row block,
+    // one workgroup per launched slot -- the count the grid below is built from
+    const uint32_t per_rb = masked ? lm.nlive : nslots;
+    if (masked) {
+        uint32_t bits = 0;
+        for (uint64_t w : lm.bits) bits += (uint32_t)__builtin_popcountll(w);
+        if (bits != lm.nlive) {
+            fprintf(stderr, "s3r: k_geometry: slot mask has %u bits but counts %u live slots\n", bits, lm.nlive);
+            abort();
+        }
+    }
+    const SkyFlags sky = gsf ? SkyFlags{gsf->flags, gsf->probe, gsf->geo_cnt, gsf->tag, gsf->gpu_eighths, gsf->err,
+                                        per_rb + gsf->extra_arrivals, device_spin_ticks()}
+                             : SkyFlags{};
     // the completion event is recorded by the launch itself (one host call instead of two)
     // dynamic LDS: one pair index per bin of a workgroup's rows (posmap)
     const uint32_t segs = fragment_segments(W), posmap_bytes = (kGeoRows / kWaves * segs + 3u) & ~3u;

@@ -63,6 +63,166 @@ using namespace s3r;
 
 namespace {
 
+// ---------------------------------------------------------------- bounded waits
+// A dlopen'ed library must never hang its caller (the reference's only failure is exit(666),
+// render.cpp:173).  Every wait of the library on a GPU has a deadline, S3R_WAIT_MS (default 30 s,
+// far above any frame: a 20 M-triangle 4K frame takes ~1 ms):
+//   * the waits on host-coherent words the kernels write (buffer-set reuse, the tile summary, the
+//     host fill's bin flags) spin with the clock in view and, past a short grace, poll the stream
+//     they are waiting on with hipStreamQuery -- finished without the word is a protocol error,
+//     unfinished at the deadline a stall;
+//   * the blocking HIP calls (stream / event / device synchronisation before frees, at frame ends,
+//     in the statistics getters) run with a watchdog armed for the call: a thread that wakes a few
+//     times a second and ends the process when an armed call has passed its deadline;
+//   * the one device-side spin (k_geometry's sky-flag publishers, kernels.hip publish_sky_flags)
+//     has a clock deadline of its own and reports through the device's error words (Dev::diag_host).
+// Expiry prints the stage, the kernel waited for, the device and the frame to stderr and ends the
+// process with status kStallExit: no retry, no re-exec, no further HIP call (_exit: the runtime's
+// exit handlers would wait for the same queue).
+int wait_deadline_ms() {
+    static const int ms = [] {
+        const char *e = getenv("S3R_WAIT_MS");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? (int)std::min<long>(v, 3600000L) : 30000;
+    }();
+    return ms;
+}
+
+int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct WaitSite {
+    const char *stage;      // what the library was doing
+    const char *kernel;     // what it waited for
+    int device;
+    uint32_t frame;
+};
+
+[[noreturn]] void stall_exit(const WaitSite &w, const char *how, double waited_ms) {
+    fprintf(stderr, "s3r: stall: %s -- waited %.0f ms for %s (%s; device %d, frame %u, S3R_WAIT_MS %d); exiting with "
+            "status %d\n", w.stage, waited_ms, w.kernel, how, w.device, w.frame, wait_deadline_ms(), kStallExit);
+    fflush(stderr);
+    _exit(kStallExit);
+}
+
+[[noreturn]] void fault_exit(const WaitSite &w, hipError_t e) {
+    fprintf(stderr, "s3r: HIP error %s while waiting for %s (%s; device %d, frame %u)\n", hipGetErrorName(e), w.kernel,
+            w.stage, w.device, w.frame);
+    fflush(stderr);
+    abort();
+}
+
+// The watchdog: one slot per thread that makes blocking HIP calls (the caller's thread and the
+// device workers), armed with a deadline and the call's site for the duration of the call.
+class Watchdog {
+  public:
+    struct Guard {
+        Guard(const WaitSite &w) : slot_(instance().arm(w)) {}
+        ~Guard() { instance().disarm(slot_); }
+        int slot_;
+    };
+    static Watchdog &instance() {
+        static Watchdog *w = new Watchdog();   // never destroyed: the thread outlives static teardown
+        return *w;
+    }
+
+  private:
+    static constexpr int kSlots = 128;
+    struct Slot {
+        std::atomic<int64_t> deadline{0};      // 0: disarmed
+        std::atomic<int64_t> start{0};
+        WaitSite site{"", "", -1, 0};
+        std::atomic<bool> used{false};
+    };
+    Slot slots_[kSlots];
+    std::once_flag started_;
+
+    // this thread's slot, taken on its first armed call and returned when the thread ends
+    struct Owner {
+        int idx = -1;
+        ~Owner() { if (idx >= 0) instance().slots_[idx].used.store(false, std::memory_order_release); }
+    };
+    int my_slot() {
+        thread_local Owner o;
+        if (o.idx < 0) {
+            for (int i = 0; i < kSlots && o.idx < 0; i++) {
+                bool f = false;
+                if (slots_[i].used.compare_exchange_strong(f, true, std::memory_order_acq_rel)) o.idx = i;
+            }
+            if (o.idx < 0) {
+                fprintf(stderr, "s3r: watchdog: more than %d threads wait on the GPU at once\n", kSlots);
+                abort();
+            }
+        }
+        return o.idx;
+    }
+    int arm(const WaitSite &w) {
+        std::call_once(started_, [this] { std::thread([this] { run(); }).detach(); });
+        const int i = my_slot();
+        Slot &s = slots_[i];
+        s.site = w;
+        const int64_t now = mono_ns();
+        s.start.store(now, std::memory_order_relaxed);
+        s.deadline.store(now + (int64_t)wait_deadline_ms() * 1000000, std::memory_order_release);
+        return i;
+    }
+    void disarm(int i) { slots_[i].deadline.store(0, std::memory_order_release); }
+    [[noreturn]] void run() {
+        const int period_ms = std::max(2, std::min(250, wait_deadline_ms() / 8));
+        for (;;) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(period_ms));
+            const int64_t now = mono_ns();
+            for (Slot &s : slots_) {
+                const int64_t d = s.deadline.load(std::memory_order_acquire);
+                if (d && now > d) {
+                    const WaitSite w = s.site;    // (its thread is blocked in the call: the site is stable)
+                    stall_exit(w, "a blocking HIP call did not return",
+                               (double)(now - s.start.load(std::memory_order_relaxed)) / 1e6);
+                }
+            }
+        }
+    }
+};
+
+// Blocking synchronisations under the watchdog.
+void sync_device(const char *stage, int device = -1, uint32_t frame = 0) {
+    Watchdog::Guard guard(WaitSite{stage, "every kernel and copy of the device", device, frame});
+    HIPCHECK(hipDeviceSynchronize());
+}
+void sync_stream(hipStream_t st, const WaitSite &w) {
+    Watchdog::Guard guard(w);
+    HIPCHECK(hipStreamSynchronize(st));
+}
+void sync_event(hipEvent_t ev, const WaitSite &w) {
+    Watchdog::Guard guard(w);
+    HIPCHECK(hipEventSynchronize(ev));
+}
+
+// One poll of a stream the host is spinning on: true when it has drained (a device fault ends the
+// process with its name), a stall exit once `t0` is past the deadline.
+bool stream_drained(hipStream_t st, const WaitSite &w, int64_t t0) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return true;
+    if (e != hipErrorNotReady) fault_exit(w, e);
+    const int64_t waited = mono_ns() - t0;
+    if (waited > (int64_t)wait_deadline_ms() * 1000000) stall_exit(w, "its stream never drained", (double)waited / 1e6);
+    return false;
+}
+
+// Test hooks for the deadline tests (tests/test_stall.py), read once, acting from a device's second
+// frame on (the first one initialises the library): S3R_TEST_HOLD_MS puts a kernel that spins that
+// long (and then exits) in front of every frame's geometry / tile setup; S3R_TEST_ARRIVALS_EXTRA
+// makes the sky-flag publishers wait for that many arrivals more than the launch has.
+uint32_t env_u32(const char *name) {
+    const char *e = getenv(name);
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint32_t)std::min<long>(v, 60000L) : 0u;
+}
+uint32_t test_hold_ms() { static const uint32_t v = env_u32("S3R_TEST_HOLD_MS"); return v; }
+uint32_t test_extra_arrivals() { static const uint32_t v = env_u32("S3R_TEST_ARRIVALS_EXTRA"); return v; }
+
 struct TimingSlot { hipEvent_t frame0, geo1, frag0, frag1; };   // geo1: the frame's geometry / setup stage done
 
 // Per-frame buffer sets in flight: frame k's geometry writes set k % kSets once the fragment kernel
@@ -170,6 +330,9 @@ struct Dev {
     // (either path)
     volatile uint32_t *done_host = nullptr;
     uint32_t *done_dev = nullptr;
+    // kDiagWords device error words (host-coherent, in done_host's allocation): a device spin that
+    // passed its deadline reports there (s3r_kernels.h GeoSkyFlags::err)
+    uint32_t *diag_host = nullptr, *diag_dev = nullptr;
     uint32_t *geo_cnt = nullptr;             // host fill: per buffer set, k_geometry's bin-phase count
     uint32_t issued_tag[kSets] = {}, last_tag = 0;
     // the previous frame's stream; NULL is a valid caller stream (the legacy default stream), so
@@ -568,10 +731,14 @@ void dev_init(Dev &d, const HostScene &s) {
     }
     {
         void *h = nullptr;
-        HIPCHECK(hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-        memset(h, 0, sizeof(uint32_t));
+        // word 0: the completion tag (wait_set_free); words 4 .. 4 + kDiagWords: the error words
+        constexpr size_t kWords = 4 + kDiagWords;
+        HIPCHECK(hipHostMalloc(&h, kWords * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+        memset(h, 0, kWords * sizeof(uint32_t));
         d.done_host = static_cast<volatile uint32_t *>(h);
         HIPCHECK(hipHostGetDevicePointer((void **)&d.done_dev, h, 0));
+        d.diag_host = static_cast<uint32_t *>(h) + 4;
+        d.diag_dev = d.done_dev + 4;
         HIPCHECK(hipEventCreateWithFlags(&d.handoff, hipEventDisableTiming));
     }
     // geometry streams at the highest priority: their (small, latency-bound) workgroups are
@@ -657,9 +824,9 @@ void initialize() {
 void drain_devices() {
     for (Dev *d : g.devs) {
         HIPCHECK(hipSetDevice(d->device));
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("drain: every device before host registrations go", d->device, d->frame_no);
     }
-    if (g.devs.empty()) HIPCHECK(hipDeviceSynchronize());
+    if (g.devs.empty()) sync_device("drain: the device before host registrations go");
     else HIPCHECK(hipSetDevice(g.devs[0]->device));
 }
 
@@ -712,7 +879,11 @@ void release_all() {
         // context is unusable after it) rather than in whatever HIP call comes next
         for (Dev *d : g.devs) {
             hipError_t e = hipSetDevice(d->device);
-            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e == hipSuccess) {
+                Watchdog::Guard guard(WaitSite{"release: draining the device", "every kernel of the device", d->device,
+                                               d->frame_no});
+                e = hipDeviceSynchronize();
+            }
             if (e != hipSuccess) {
                 fprintf(stderr, "s3r: HIP error %s on device %d while releasing the library: a fault of an "
                         "earlier frame's kernels (run with S3R_CHECK=1 to name the launch)\n", hipGetErrorName(e),
@@ -794,10 +965,10 @@ TimingSlot *timing_slot(Dev &d) {
 constexpr uint32_t kTagLimit = 0xFFFFFF00u;
 
 void restart_tags(Dev &d, uint32_t next_frame_no) {
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("frame-tag restart", d.device, d.frame_no);
     for (int p = 0; p < kSets; p++)
         if (d.bincnt[p]) HIPCHECK(hipMemset(d.bincnt[p], 0, d.bins_cap * sizeof(uint32_t)));
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("frame-tag restart: bin counts cleared", d.device, d.frame_no);
     d.frame_no = next_frame_no;
     if (d.tile_sum_host) memset(d.tile_sum_host, 0, kSumWords * kSets * sizeof(uint32_t));   // (tags restart)
     for (uint32_t &t : d.issued_tag) t = 0;
@@ -820,18 +991,23 @@ uint32_t next_set(Dev &d) {
 void wait_set_free(Dev &d, uint32_t p) {
     const uint32_t want = d.issued_tag[p];
     if (want == 0 || __atomic_load_n(d.done_host, __ATOMIC_ACQUIRE) >= want) return;
+    const WaitSite w{"row path: buffer set reuse (its last reader, an earlier frame's fragment launch)", "k_fragment",
+                     d.device, d.frame_no};
+    const int64_t t0 = mono_ns();
     if (want == d.last_tag) {
         // no row-path fragment launch after it to report it (tile-path frames followed): drain its stream
-        HIPCHECK(hipStreamSynchronize(d.last_stream));
+        while (!stream_drained(d.last_stream, w, t0)) sched_yield();
         __atomic_store_n(d.done_host, want, __ATOMIC_RELEASE);
         return;
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(d.done_host, __ATOMIC_ACQUIRE) < want) {
+    // the later launch that reports it is issued; after a grace of spinning, the previous frame's
+    // stream (every earlier frame is ordered before it, follow_previous_frame) is polled as well:
+    // drained means every reader is done even if the report was somehow missed
+    for (uint32_t k = 1; __atomic_load_n(d.done_host, __ATOMIC_ACQUIRE) < want; k++) {
         __builtin_ia32_pause();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-            HIPCHECK(hipDeviceSynchronize());      // (never expected) surfaces a device fault
+        if ((k & 1023u) == 0 && mono_ns() - t0 > 2000000 && stream_drained(d.last_stream, w, t0)) {
             __atomic_store_n(d.done_host, d.last_tag, __ATOMIC_RELEASE);
+            return;
         }
     }
 }
@@ -999,7 +1175,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     // -> 4 672-4 696 with the bins (profiles/r04_part8_ab.txt); the split launches are gone (round 5)
     const size_t npx = (size_t)W * rows_local;
     if (d.deferred_cap < npx) {                // pixels whose winner needs its full setup
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("tile path: growing the deferred-pixel buffer", d.device, d.frame_no);
         if (d.deferred) HIPCHECK(hipFree(d.deferred));
         d.deferred = dalloc<uint4>(npx);
         d.deferred_cap = npx;
@@ -1015,7 +1191,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
 
 void grow_tile_list(Dev &d, uint32_t p, uint64_t total) {
     if (d.tile_list_cap[p] >= total && d.tile_list_cap[p] > 0) return;
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("tile path: growing the tile lists", d.device, d.frame_no);
     if (d.tile_list[p]) HIPCHECK(hipFree(d.tile_list[p]));
     // a quarter of headroom (S3R_TILE_LIST_EXACT=1, tests: none, so the next larger frame overflows)
     const bool exact = getenv("S3R_TILE_LIST_EXACT") && atoi(getenv("S3R_TILE_LIST_EXACT")) != 0;
@@ -1034,15 +1210,17 @@ bool bins_on(const Dev &d);
 
 void wait_tile_summary(Dev &d, uint32_t p, hipStream_t geo) {
     volatile uint32_t *sum = d.tile_sum_host + kSumWords * p;
-    const auto t0 = std::chrono::steady_clock::now();
+    const WaitSite w{"tile path: the frame's setup summary (list and bin sizes)", "k_tile_setup / k_tile_cursor",
+                     d.device, d.frame_no};
+    const int64_t t0 = mono_ns();
     for (uint32_t k = 1; __atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no; k++) {
         __builtin_ia32_pause();
-        if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-            HIPCHECK(hipStreamSynchronize(geo));
-            if (__atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no) {
-                fprintf(stderr, "s3r: tile path: the frame's summary never arrived\n");
-                abort();
-            }
+        if ((k & 255u) == 0 && mono_ns() - t0 > 2000000 && stream_drained(geo, w, t0) &&
+            __atomic_load_n(&sum[0], __ATOMIC_ACQUIRE) != d.frame_no) {
+            fprintf(stderr, "s3r: tile path: the setup of frame %u finished on device %d without its summary "
+                    "(buffer set %u carries tag %u)\n", d.frame_no, d.device, p, (unsigned)sum[0]);
+            fflush(stderr);
+            abort();
         }
     }
     // (bins mode: word 2, the binned entries, is written by the frame's last kernel, after this
@@ -1065,17 +1243,17 @@ bool bins_on(const Dev &d) { return g.tile_bins && !d.bins_off; }
 // only the tile path renders; the lists' 16-B live entries are 2.6 GB that bins mode never touches).
 void ensure_row_sets(Dev &d) {
     if (d.tris[0]) return;
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("row path: first frame, TriSetup records", d.device, d.frame_no);
     for (int p = 0; p < kSets; p++) d.tris[p] = dalloc<TriSetup>(2 * (size_t)g.ntri);
 }
 void ensure_live(Dev &d) {
     if (d.live[0]) return;
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("tile path: live-entry lists", d.device, d.frame_no);
     for (int p = 0; p < kSets; p++) d.live[p] = dalloc<uint4>((size_t)2 * g.ntri);
 }
 
 void drop_bins(Dev &d) {
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("tile path: dropping the bins", d.device, d.frame_no);
     for (int q = 0; q < kSets; q++) {
         if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
         d.tbin[q] = nullptr;
@@ -1095,7 +1273,7 @@ void ensure_bins(Dev &d, uint64_t nt) {
     }
     for (int q = 0; q < kSets; q++) {
         if (d.tbin[q] && d.tbin_slots[q] >= nt) continue;
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("tile path: allocating the bins", d.device, d.frame_no);
         if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
         d.tbin[q] = dalloc<uint32_t>(nt * d.bin_cap);
         d.tbin_slots[q] = nt;
@@ -1112,7 +1290,7 @@ bool grow_bins(Dev &d, uint32_t need) {
         drop_bins(d);
         return false;
     }
-    HIPCHECK(hipDeviceSynchronize());
+    sync_device("tile path: growing the bins", d.device, d.frame_no);
     for (int q = 0; q < kSets; q++) {
         if (d.tbin[q]) HIPCHECK(hipFree(d.tbin[q]));
         d.tbin[q] = dalloc<uint32_t>(d.tbin_slots[q] * cap);
@@ -1144,7 +1322,7 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
         rebin(d, p, d.tile_W, d.tile_H, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, geo);
         tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
                             nullptr, d.tile_frame_rows);
-        HIPCHECK(hipStreamSynchronize(st));
+        sync_stream(st, WaitSite{"tile path: an overflowed frame binned and rendered again", "k_tile_raster", d.device, d.frame_no});
         return true;
     }
     if (total <= d.tile_list_cap[p]) return false;
@@ -1155,7 +1333,7 @@ bool tile_redo_if_overflowed(Dev &d, hipStream_t st) {
                        d.tile_xoff);
     tile_fragment_stage(d, p, d.tile_W, d.tile_band, d.tile_nparts, d.tile_part, d.tile_rows, d.tile_out, geo, st,
                         nullptr, d.tile_frame_rows);
-    HIPCHECK(hipStreamSynchronize(st));
+    sync_stream(st, WaitSite{"tile path: an overflowed frame listed and rendered again", "k_tile_raster", d.device, d.frame_no});
     return true;
 }
 
@@ -1201,7 +1379,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     d.tile_xoff = frame_rows && g.tile_line_grid && W % 16u == 0u ? (uint32_t)(((uintptr_t)out >> 2) & 15u) : 0u;
     const uint64_t nt = tile_slots(W, rows_local, d.tile_xoff);   // (tile, depth bucket) entries
     if (d.tiles_cap < nt) {
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("tile path: growing the tile counters", d.device, d.frame_no);
         for (int p = 0; p < kSets; p++) {
             for (uint32_t **q : {&d.tile_counts[p], &d.tile_offs[p], &d.tile_cursor[p]}) {
                 if (*q) HIPCHECK(hipFree(*q));
@@ -1211,7 +1389,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
             // memset does not order the geometry streams, hence the synchronisation
             HIPCHECK(hipMemset(d.tile_counts[p], 0, nt * sizeof(uint32_t)));
         }
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("tile path: tile counters zeroed", d.device, d.frame_no);
         if (d.scan_temp) HIPCHECK(hipFree(d.scan_temp));
         d.scan_temp_bytes = tile_scan_temp_bytes(nt);
         d.scan_temp = dalloc<uint8_t>(d.scan_temp_bytes);
@@ -1225,7 +1403,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (vs_env ? atoi(vs_env) != 0 : nparts > 1 && !tile_clusters(d, nparts).ncl) {
         if (!d.vrv) d.vrv = dalloc<float4>(g.nv);
     } else if (d.vrv) {
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("tile path: dropping the vertex stage", d.device, d.frame_no);
         HIPCHECK(hipFree(d.vrv));
         d.vrv = nullptr;
     }
@@ -1241,7 +1419,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
                                hipHostMallocCoherent | hipHostMallocMapped));
         memset(d.tile_sum_host, 0, kSumWords * kSets * sizeof(uint32_t));
         HIPCHECK(hipHostGetDevicePointer((void **)&d.tile_sum_dev, d.tile_sum_host, 0));
-        HIPCHECK(hipDeviceSynchronize());          // (the null-stream memsets vs the geometry streams)
+        sync_device("tile path: first frame, summary words", d.device, d.frame_no);          // (the null-stream memsets vs the geometry streams)
     }
     const uint32_t p = next_set(d);
     hipStream_t geo = d.geo[0];
@@ -1263,6 +1441,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
         g.env_tile_norec = e ? atoi(e) : 1;
     }
     d.tile_norec = g.env_tile_norec == 1 || (frame_rows && g.env_tile_norec == 2);
+    if (test_hold_ms() && d.frame_no >= 2) launch_test_hold(test_hold_ms(), geo);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
@@ -1341,7 +1520,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     fragment_configure(W, rows_local);
     const size_t need = (size_t)2 * g.ntri * rows_local * start_entries(W) * 4;
     if (d.rowtab_cap < need) {
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("row path: growing the start table", d.device, d.frame_no);
         for (int p = 0; p < kSets; p++) {
             if (d.rowtab[p]) HIPCHECK(hipFree(d.rowtab[p]));
             d.rowtab[p] = dalloc<float>(need);
@@ -1350,7 +1529,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     }
     const uint64_t nbins = fragment_bins(W, rows_local);
     if (d.bins_cap < nbins) {
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("row path: growing the bins", d.device, d.frame_no);
         for (int p = 0; p < kSets; p++) {
             if (d.bincnt[p]) HIPCHECK(hipFree(d.bincnt[p]));
             if (d.pairs[p]) HIPCHECK(hipFree(d.pairs[p]));
@@ -1360,7 +1539,7 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
         }
         // hipMemset runs on the null stream, which does not order the non-blocking geometry
         // streams: finish it before the next k_geometry counts pairs in these bins
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("row path: bin counts zeroed", d.device, d.frame_no);
         d.bins_cap = nbins;
     }
     // longest-first order only where a launch is more than one round of resident workgroups (~1 280
@@ -1379,13 +1558,13 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     const bool lpt = g.ntri > 0 && !hf && bins >= (lpt_env ? strtoull(lpt_env, nullptr, 10) : kLptMinBins) &&
                      (lpt_env || fragment_segment_pixels() >= 384u);     // (6 chunks of 64 px)
     if (lpt && d.order_cap < bins) {
-        HIPCHECK(hipDeviceSynchronize());
+        sync_device("row path: growing the order column", d.device, d.frame_no);
         for (int q = 0; q < kSets; q++) {
             if (d.order[q]) HIPCHECK(hipFree(d.order[q]));
             d.order[q] = dalloc<uint32_t>(2 * bins);
             HIPCHECK(hipMemset(d.order[q], 0, 2 * bins * sizeof(uint32_t)));
         }
-        HIPCHECK(hipDeviceSynchronize());     // (as for the bin counts: before k_geometry writes perm)
+        sync_device("row path: order column zeroed", d.device, d.frame_no);     // (as for the bin counts: before k_geometry writes perm)
         d.order_cap = bins;
     }
     // geometry for this frame into buffer set p, once the fragment kernel that last read set p is done
@@ -1414,11 +1593,12 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
         if (!d.geo_cnt) {
             d.geo_cnt = dalloc<uint32_t>((size_t)kSets * kGeoCounterWords);
             HIPCHECK(hipMemset(d.geo_cnt, 0, (size_t)kSets * kGeoCounterWords * sizeof(uint32_t)));
-            HIPCHECK(hipDeviceSynchronize());      // (null-stream memset: finish before the geometry stream)
+            sync_device("row path: geometry counters zeroed", d.device, d.frame_no);      // (null-stream memset: finish before the geometry stream)
         }
         gsf = GeoSkyFlags{hf->flags_dev, hf->probe_dev, d.geo_cnt + (size_t)p * kGeoCounterWords, hf->tag,
-                          hf->gpu_eighths};
+                          hf->gpu_eighths, d.diag_dev, d.frame_no >= 2 ? test_extra_arrivals() : 0u};
     }
+    if (test_hold_ms() && d.frame_no >= 2) launch_test_hold(test_hold_ms(), geo);
     launch_geometry(d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, W, H, band, nparts, part,
                     rows_local, d.tris[p], d.rowtab[p], d.bincnt[p], d.pairs[p], geo, chained ? nullptr : d.geo_done[p],
                     lpt ? d.order[p] : nullptr, gsf.flags ? &gsf : nullptr, row_starts, g.clip_slots, &g.live);
@@ -1612,7 +1792,7 @@ void deliver_part(void *arg, int i) {
             copy_bands_to_host(d.frame, job.W, job.H, job.band, job.nparts, (uint32_t)i, job.host, d.stream);
         }
     }
-    HIPCHECK(hipStreamSynchronize(d.stream));
+    sync_stream(d.stream, WaitSite{"updateAndRender: the frame part rendered and copied to the caller", "the frame's kernels and copy", d.device, d.frame_no});
     if (rows && job.W && tile_redo_if_overflowed(d, d.stream)) {
         // the tile list was too short for this frame: rendered again, delivered again
         if (job.nparts == 1) {
@@ -1621,7 +1801,7 @@ void deliver_part(void *arg, int i) {
         } else {
             copy_bands_to_host(d.frame, job.W, job.H, job.band, job.nparts, (uint32_t)i, job.host, d.stream);
         }
-        HIPCHECK(hipStreamSynchronize(d.stream));
+        sync_stream(d.stream, WaitSite{"updateAndRender: the frame part rendered and copied to the caller", "the frame's kernels and copy", d.device, d.frame_no});
     }
     note_device_done(i, job.nparts == 1 ? job.copy_bytes : (uint64_t)rows * job.W * 4);
 }
@@ -1835,6 +2015,8 @@ struct FillPart {
     unsigned long long *chunks;      // host view of its covered bins' chunk masks
     uint32_t tag, seg_px, segs, rpb, chunk_px, rows_local, band, nparts, part;
     uint64_t bins;
+    const uint32_t *diag;            // the device's error words (Dev::diag_host)
+    int device;
 };
 
 struct FillJob {
@@ -1853,6 +2035,7 @@ struct FillJob {
     std::atomic<uint64_t> sky_bins{0};
     std::atomic<uint64_t> part_px[kMaxDevices] = {};   // per part, as sky_px
     int64_t issued_ns = 0;                                 // part 0's launches issued
+    std::atomic<int> parts_done{0};                        // device parts synchronised
     std::chrono::steady_clock::time_point dev_done_ns[kMaxDevices];   // each device part's end
     int64_t thread_end_ns[65] = {};  // per fill thread (written by that thread, read after the join)
     uint64_t thread_px[65] = {};
@@ -1900,6 +2083,34 @@ uint64_t fill_bin(const FillJob &job, const FillPart &fp, uint64_t b, bool sky, 
 // filled whole; a covered bin waits for its workgroup's chunk mask (end of the workgroup) and gets
 // the row chunks without a winner filled.
 constexpr uint64_t kWaitChunks = 1ull << 47;    // pending entry: sky flag seen, covered, mask awaited
+
+// A fill thread still waiting for flags or chunk masks (bounded waits, above): a sky-flag publisher
+// that timed out on its device ends the process at once, naming its row block and arrival count;
+// past the deadline, a frame whose device parts have all been synchronised is a flag protocol error,
+// and one whose parts are still running a stall (the parts' own waits are bounded by the watchdog).
+void fill_check(const FillJob &job, size_t waiting, std::chrono::steady_clock::time_point t0) {
+    for (int p = 0; p < job.nparts; p++) {
+        const uint32_t *e = job.parts[p].diag;
+        if (e && __atomic_load_n(e, __ATOMIC_ACQUIRE) == kDiagPublisherTimeout) {
+            fprintf(stderr, "s3r: stall: host fill -- k_geometry's sky-flag publisher of row block %u timed out on device "
+                    "%d (frame tag %u): %u of %u geometry workgroups arrived within S3R_SPIN_MS; exiting with status %d\n",
+                    __atomic_load_n(e + 1, __ATOMIC_ACQUIRE), job.parts[p].device, job.parts[p].tag,
+                    __atomic_load_n(e + 2, __ATOMIC_ACQUIRE), __atomic_load_n(e + 3, __ATOMIC_ACQUIRE), kStallExit);
+            fflush(stderr);
+            _exit(kStallExit);
+        }
+    }
+    const double waited_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (waited_ms <= wait_deadline_ms()) return;
+    const WaitSite w{"host fill: the frame's bin flags and chunk masks", "k_geometry's publishers / k_fragment",
+                     job.parts[0].device, job.parts[0].tag};
+    if (job.parts_done.load(std::memory_order_acquire) == job.nparts) {
+        fprintf(stderr, "s3r: host fill: %zu bins never flagged although every device part finished (flag protocol "
+                "broken)\n", waiting);
+        stall_exit(w, "every device part finished", waited_ms);
+    }
+    stall_exit(w, "device parts still running", waited_ms);
+}
 
 void fill_worker(void *arg, int idx) {
     FillJob &job = *static_cast<FillJob *>(arg);
@@ -1961,12 +2172,7 @@ void fill_worker(void *arg, int idx) {
         }
         if (keep == n) {
             __builtin_ia32_pause();
-            if ((++idle & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
-                // every device part has been synchronised by the time a frame takes this long, so a
-                // bin never flagged is a protocol bug, not a slow device: fail loudly
-                fprintf(stderr, "s3r: host fill: %zu bins never flagged in 20 s (flag protocol broken)\n", keep);
-                abort();
-            }
+            if ((++idle & 4095u) == 0) fill_check(job, keep, t0);
         }
         n = keep;
     }
@@ -2026,9 +2232,10 @@ void deliver_part_direct(void *arg, int i) {
     }
     if (i == 0)
         job.issued_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - job.t0).count();
-    HIPCHECK(hipStreamSynchronize(d.stream));
+    sync_stream(d.stream, WaitSite{"updateAndRender: the frame part written into the caller's buffer", "the frame's kernels", d.device, d.frame_no});
     // a tile-path frame whose list overflowed is rendered again, into the same rows
     if (fp.rows_local && job.W) tile_redo_if_overflowed(d, d.stream);
+    job.parts_done.fetch_add(1, std::memory_order_acq_rel);
     note_end(job, job.dev_end_ns);
     job.dev_done_ns[i] = std::chrono::steady_clock::now();
 }
@@ -2103,6 +2310,8 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
         fp.seg_px = l.seg_px; fp.segs = l.segs; fp.rpb = l.rows_per_bin; fp.chunk_px = l.chunk_px;
         fp.bins = fp.rows_local ? l.bins : 0;
         fp.band = band; fp.nparts = nparts; fp.part = i;
+        fp.diag = g.devs[i]->diag_host;
+        fp.device = g.devs[i]->device;
     }
     for (uint32_t i = 0; i < nparts; i++) {
         Dev &d = *g.devs[i];
@@ -2183,12 +2392,22 @@ MappedResult mapped_frame(uint32_t *buffer, uint32_t W, uint32_t H, uint32_t ban
 // kernel; the statistics read it once the device is drained.
 void refresh_pairs(Dev &d) {
     if (d.last_path != 2 || !d.last_set_bins || d.last_set < 0 || !d.tile_sum_host) return;
+    // only the last tile frame's fragment stage, and the caller's current device left as it was
+    int prev = -1;
+    HIPCHECK(hipGetDevice(&prev));
     HIPCHECK(hipSetDevice(d.device));
-    HIPCHECK(hipDeviceSynchronize());
+    sync_event(d.frag_done[d.last_set], WaitSite{"statistics: the last tile frame", "k_tile_raster", d.device, d.frame_no});
     d.last_pairs = __atomic_load_n(d.tile_sum_host + kSumWords * (uint32_t)d.last_set + 2, __ATOMIC_ACQUIRE);
+    HIPCHECK(hipSetDevice(prev));
 }
 
 }  // namespace
+
+namespace s3r {
+void sync_stream_bounded(hipStream_t st, const char *stage, const char *kernel, int device, uint32_t frame) {
+    sync_stream(st, WaitSite{stage, kernel, device, frame});
+}
+}  // namespace s3r
 
 extern "C" {
 
@@ -2371,7 +2590,7 @@ __attribute__((visibility("default"))) void s3r_unregister_host(void *ptr) {
             if (g.initialized) drain_devices();
             else {
                 if (g.device >= 0) HIPCHECK(hipSetDevice(g.device));
-                HIPCHECK(hipDeviceSynchronize());          // no copy into it may still be in flight
+                sync_device("s3r_unregister_host: before the registration goes", g.device);          // no copy into it may still be in flight
             }
         }
         unregister_range(g.regs[i]);
@@ -2459,7 +2678,7 @@ __attribute__((visibility("default"))) void s3r_timing_stages(double out[4]) {
         HIPCHECK(hipSetDevice(d.device));
         for (size_t i = 0; i < d.tcount; i++) {
             float a = 0, b = 0, c = 0;
-            HIPCHECK(hipEventSynchronize(d.tslots[i].frag1));
+            sync_event(d.tslots[i].frag1, WaitSite{"s3r_timing_stages", "a timed frame", d.device, d.frame_no});
             HIPCHECK(hipEventElapsedTime(&a, d.tslots[i].frag0, d.tslots[i].frag1));
             HIPCHECK(hipEventElapsedTime(&b, d.tslots[i].frame0, d.tslots[i].frag1));
             HIPCHECK(hipEventElapsedTime(&c, d.tslots[i].frame0, d.tslots[i].geo1));

@@ -14,6 +14,17 @@ bool check_launches();
 void check_context(int device, uint32_t frame, const char *stage);
 void after_launch(const char *kernel, hipStream_t st);
 
+// Bounded waits (render_api.cpp "bounded waits"): a wait past its deadline (S3R_WAIT_MS) prints
+// its stage, kernel, device and frame and ends the process with this status.
+constexpr int kStallExit = 86;
+// hipStreamSynchronize under the library's watchdog (what after_launch uses)
+void sync_stream_bounded(hipStream_t st, const char *stage, const char *kernel, int device, uint32_t frame);
+// Test hook (S3R_TEST_HOLD_MS): a one-wave kernel that spins `ms` milliseconds of the device clock
+// and exits -- a stage that is late but always finishes, for the deadline tests.
+void launch_test_hold(uint32_t ms, hipStream_t st);
+// The clock-tick budget of the device spins (S3R_SPIN_MS, default 2000 ms; 100 MHz ticks).
+uint32_t device_spin_ticks();
+
 // `done` (may be null): recorded on `st` when the launched kernel completes.
 // order (may be null: launch order): 2 x fragment_bins() words, [perm | cost] -- launch_geometry's
 // extra workgroup (order non-null there) writes perm, the launch's workgroup -> bin map, from the
@@ -56,9 +67,16 @@ uint32_t start_entries(uint32_t W);
 // workgroup's pair reservations are in (see launch_sky_flags for flags / tag / probe / gpu_eighths);
 // geo_cnt: kGeoCounterWords zeroed device words (the launch leaves them 0), one set per launch in flight.
 constexpr uint32_t kGeoCounterWords = 256 * 16;
+// err: kDiagWords host-coherent words (Dev::diag_host) -- a publisher whose spin passes its clock
+// deadline stores {kDiagPublisherTimeout, row block, arrivals seen, arrivals expected} there and
+// returns without publishing (the host reports it; render_api.cpp fill_worker).  extra_arrivals: a
+// test hook (S3R_TEST_ARRIVALS_EXTRA) added to the arrivals the publishers wait for.
+constexpr uint32_t kDiagWords = 4, kDiagPublisherTimeout = 1;
 struct GeoSkyFlags {
     uint32_t *flags, *probe, *geo_cnt;
     uint32_t tag, gpu_eighths;
+    uint32_t *err;
+    uint32_t extra_arrivals;
 };
 // clip_slots = false: no triangle can cross the near plane this frame (the host's check,
 // render_api.cpp near_plane_crossing), so the launch leaves out the clip-appended slots T..2T-1 (their

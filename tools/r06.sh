@@ -1,0 +1,92 @@
+#!/bin/bash
+# Round-6 experiments on the GPU box, one recipe per call:  bash tools/r06.sh <recipe> [<recipe> ...]
+# Every step writes its stdout AND stderr to its own file under gpurun_out/r06/ (nothing discarded,
+# nothing held back in a pipe, so a stalled step leaves what it printed), runs under its own time limit,
+# and a failing step ends the call (no retries).  Variant libraries come from tools/variants.py build.
+OUT=gpurun_out/r06
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STRESS=/tmp/s3r_stress.bin
+
+step() {   # step <name> <seconds> <command...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T)): $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"
+  tail -n 4 "$OUT/$name.log"
+  return $rc
+}
+
+bench_line() {   # bench_line <name> <env...> -- the bench workload, one JSON line kept in <name>.json
+  local name=$1; shift
+  step "$name" 150 env "$@" python3 -u bench.py --steps 400 --warmup 40 --no-cpu-baseline || return 1
+  grep '^{' "$OUT/$name.log" | tail -1 > "$OUT/$name.json"
+  python3 -c "import json; d=json.load(open('$OUT/$name.json')); print('  $name', round(d['value']), 'fps  device', round(d['device_fps']), 'frag_ms', d['fragment_kernel_ms'])"
+}
+
+part8() {   # part8 <name> <env...> -- part 0 of an 8-way band split of the bench frame, pipelined
+  local name=$1; shift
+  step "$name" 150 env "$@" python3 -u tools/overhead_probe.py --nparts 8 --steps 2000 || return 1
+  python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/$name.log') if l.startswith('{')][-1]
+print('  $name part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 2))"
+}
+
+kstats() {   # kstats <name> <env...> -- rocprofv3 kernel averages of the bench workload
+  local name=$1; shift
+  step "$name" 200 env "$@" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o run -- \
+      python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline || return 1
+  local f
+  f=$(find "$OUT/$name" -name '*kernel_stats.csv' | sort | tail -1)
+  python3 - "$f" <<'EOF'
+import csv, sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:6]:
+    print('  %-58s %7s calls  avg %8.2f us' % (r['Name'][:58], r['Calls'], float(r['AverageNs']) / 1e3))
+EOF
+}
+
+lds_pmc() {   # lds_pmc <name> <env...> -- LDS counters of the bench workload's kernels
+  local name=$1; shift
+  step "$name" 120 env "$@" rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS \
+      SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d "$OUT/$name" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-device || return 1
+  python3 tools/pmc_summary.py "$OUT/$name" --last 10 > "$OUT/$name.summary.txt" 2>&1 || return 1
+  python3 - "$OUT/$name/pmc_summary.json" <<'EOF2'
+import json, sys
+for k, c in json.load(open(sys.argv[1])).items():
+    if 'k_fragment' in k or 'k_geometry' in k:
+        print('  %-44s conflict/active %.3f  lds-wait/wave-cycles %.3f  stall %.3f  VALU %.3g SALU %.3g LDS %.3g' % (
+            k[-44:], c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_LDS_IDX_ACTIVE'], 1), c['SQ_WAIT_INST_LDS'] / max(c['SQ_WAVE_CYCLES'], 1),
+            c['SQ_WAIT_INST_ANY'] / max(c['SQ_WAVE_CYCLES'], 1), c['SQ_INSTS_VALU'], c['SQ_INSTS_SALU'], c['SQ_INSTS_LDS']))
+EOF2
+}
+
+for recipe in "$@"; do
+  case $recipe in
+    tabpad)   # padded table rows (product) vs the round-5 layout (S3R_TAB_PAD=0 build)
+      for i in 1 2; do
+        bench_line tabpad_bench_pad$i || exit 1
+        bench_line tabpad_bench_pad0_$i S3R_LIB=build/librender_pad0.so || exit 1
+      done
+      part8 tabpad_part8_pad || exit 1
+      part8 tabpad_part8_pad0 S3R_LIB=build/librender_pad0.so || exit 1
+      kstats tabpad_k_pad || exit 1
+      kstats tabpad_k_pad0 S3R_LIB=build/librender_pad0.so || exit 1
+      lds_pmc tabpad_pmc_pad || exit 1
+      lds_pmc tabpad_pmc_pad0 S3R_LIB=build/librender_pad0.so || exit 1
+      ;;
+    rowparity)   # the row path's parity suite
+      step rowparity 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+          tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
+      ;;
+    stall)   # the bounded-wait tests (each a child process that must end with status 86)
+      step stall 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_stall.py || exit 1
+      ;;
+    suite)   # the whole GPU suite, once
+      step suite 1100 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests || exit 1
+      ;;
+    *) echo "unknown recipe $recipe"; exit 2 ;;
+  esac
+done
