@@ -141,16 +141,35 @@ def frame_roofline(W, H, nv, ni, na, ntex, textured, device_s, delivered_s):
     return out
 
 
+def library_sha256():
+    """SHA-256 of the library this process renders with (the one renderer.load_library opened)."""
+    import hashlib
+    from swift3drenderer_amd.renderer import LIB_PATH
+    try:
+        with open(LIB_PATH, 'rb') as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def load_traffic(workload_key, field='hbm_bytes_per_launch'):
     """HBM bytes per launch (the fragment kernel's, or with field='setup_hbm_bytes_per_launch' the
-    tile path's setup) from the committed rocprofv3 --pmc summary (profiles/pmc_traffic.json)."""
+    tile path's setup) from the committed rocprofv3 --pmc summary (profiles/pmc_traffic.json,
+    tools/pmc_traffic.py) -- only when that PMC pass measured this very library (its SHA-256 recorded
+    beside the bytes): a figure from another build is not reported.  Returns (bytes, provenance)."""
     p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(workload_key, {}).get(field)
+            e = json.load(f).get(workload_key, {})
     except Exception:
-        return None
+        return None, None
+    v = e.get(field)
+    if v is None:
+        return None, None
+    if not e.get('library_sha256') or e['library_sha256'] != library_sha256():
+        return None, 'profiles/pmc_traffic.json measured another build of the library: not reported'
+    kern = e.get('setup_kernel' if field.startswith('setup') else 'kernel', '?')
+    return v, f"{e.get('source', '?')}; kernel {kern}; library sha256 {e['library_sha256'][:12]}"
 
 
 class DoubleBuffer:
@@ -560,7 +579,7 @@ def run_rank0(a, N, np, torch):
     if path == 2 and device_fps:
         # the tile path reads no per-vertex attributes beyond the winners' (§8(d)'s 48 A bytes are not its
         # traffic): the PMC-measured bytes of its setup and fused raster per frame over the device frame
-        cb = [load_traffic(workload, 'setup_hbm_bytes_per_launch'), load_traffic(workload)]
+        cb = [load_traffic(workload, 'setup_hbm_bytes_per_launch')[0], load_traffic(workload)[0]]
         if all(cb):
             frame_roof['counter_bytes_per_frame'] = int(sum(cb))
             frame_roof['counter_frac_device'] = round(sum(cb) * device_fps / 1e9 / HBM_PEAK_GBS, 5)
@@ -577,6 +596,8 @@ def run_rank0(a, N, np, torch):
         shutil.rmtree(tmp, ignore_errors=True)
 
     frame_bytes = 4 * W * H
+    traffic, traffic_src = load_traffic(workload)
+    setup_traffic, setup_src = load_traffic(workload, 'setup_hbm_bytes_per_launch')
     return {
         'metric': METRIC,
         'value': round(fps, 3),
@@ -628,16 +649,14 @@ def run_rank0(a, N, np, torch):
         # events on its stream from the frame's first launch to the stage's end, same frames as roofline
         'setup_ms': round(geo_ms / max(nfr, 1), 5),
         'setup_bytes_per_frame': (16 * nv + 4 * ni + 4 * pairs) if path == 2 else None,
-        'setup_traffic': load_traffic(workload, 'setup_hbm_bytes_per_launch') if path == 2 else None,
-        # delivered tile frames write no record for the slots the raster rebuilds (Delivered
-        # tile frames without records): their setup's PMC bytes per frame
-        'setup_traffic_delivered': load_traffic(workload, 'delivered_setup_hbm_bytes_per_launch') if path == 2 else None,
+        'setup_traffic': setup_traffic if path == 2 else None,
+        'setup_traffic_source': setup_src if path == 2 else None,
         'setup_bytes_note': ('tile path, a lower bound: vertices 16 B and indices 4 B read, a 4-B bin entry '
-                             'written per binned entry; the 48-B raster record of each live slot is not counted '
-                             '(bins mode does not count live slots); setup_traffic: device-resident frames, '
-                             'setup_traffic_delivered: delivered frames (PMC)') if path == 2 else None,
+                             'written per binned entry; the setup writes no raster record except for the clip\'s '
+                             'slots (rare; not counted); setup_traffic: the PMC bytes per frame of the same '
+                             'library (tools/pmc_traffic.py)') if path == 2 else None,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': load_traffic(workload),
+                     'frac': round(achieved / HBM_PEAK_GBS, 5), 'traffic': traffic, 'traffic_source': traffic_src,
                      'kernel': kernel, 'algorithmic_bytes_per_launch': frag_bytes,
                      'launch': roof_launch, 'frame': frame_roof},
         'cpu_baseline': cpu,

@@ -340,9 +340,6 @@ constexpr uint32_t kListMax = 5 * kTPB;
 #ifndef S3R_WORK_SKY
 #define S3R_WORK_SKY 8                 // a sky bin's work units (its fill of the background)
 #endif
-#ifndef S3R_ORDER_WALL
-#define S3R_ORDER_WALL 0               // 1: bins ordered by their measured wall time (rounds 3-4)
-#endif
 #ifndef S3R_LINE_STORES
 #define S3R_LINE_STORES 1              // HOSTW: wave stores on the caller buffer's 64-B line grid
 #endif
@@ -375,7 +372,6 @@ struct FragShared {
     uint32_t st_k[kWaves][kStateBatches * 64];
     float4 tab4[kWaves][kTables][kTabStride / 4];  // exact S(c, d, k), k < kChunk, filled by sequential adds
     uint32_t cnt, next;
-    uint32_t t_start;                    // the workgroup's start (100 MHz ticks, low 32 bits): its cost
     uint32_t bgm[kWaves];                // host fill: per wave (row), its chunks left to the host
     uint32_t wwork[kWaves];              // per wave: its work units (the bin's cost, order_bins)
 };
@@ -1041,22 +1037,27 @@ __device__ __forceinline__ void alltab_chunk(const BatchLanes &v, uint32_t lane,
         const uint64_t negm = __ballot(neg);
         const uint64_t gm = __ballot(mine);
         uint64_t live = gm & ~(negm | (negm >> 1) | (negm >> 2)) & 0x9249249249249249ull;
+        wk += kWorkTest * (uint32_t)__builtin_popcountll(live);
         while (live) {
             const uint32_t l0 = (uint32_t)__builtin_ctzll(live);
             live &= live - 1;
-            wk += kWorkTest;
             const uint32_t tk0 = rdl(v.k0, l0), txmax = rdl(v.xmax, l0), t0 = rdl(ti, l0);
             const float r0 = rdl(v.rz, l0), r1 = rdl(v.rz, l0 + 1u), r2 = rdl(v.rz, l0 + 2u);
             const int tslot = (int)rdl(v.slot, l0);
-            if (xl < tk0 || xl > txmax) continue;
-            const uint32_t off = xl - tk0;
+            // branch-free: every lane reads its table entry (a lane left of the triangle's first pixel
+            // reads entry 63, one right of its last a value past it -- both discarded by `hit`), so
+            // the wave runs no exec-mask save / restore per triangle (round 6: against the branching
+            // test 47.8 -> 47.6 us, SALU 12.9 -> 12.6 M; profiles/r06_pix_select_ab.txt)
+            const uint32_t off = min(xl - tk0, kChunk - 1u);
             const float a0 = tab[t0][off], a1 = tab[t0 + 1u][off], a2 = tab[t0 + 2u][off];
-            if (a0 >= 0 && a1 >= 0 && a2 >= 0) {                               // :362
-                const float ooz = (r0 * a0 + r1 * a1) + r2 * a2;                 // :363
-                if (ooz > depth[0]) {                                             // :364
-                    depth[0] = ooz; win[0] = tslot; bw0[0] = a0; bw1[0] = a1; bw2[0] = a2;
-                }
-            }
+            const float ooz = (r0 * a0 + r1 * a1) + r2 * a2;                     // :363
+            const bool hit = (xl >= tk0) & (xl <= txmax) & (a0 >= 0) & (a1 >= 0) & (a2 >= 0)   // :362
+                             & (ooz > depth[0]);                                 // :364 (& not &&: no branches)
+            depth[0] = hit ? ooz : depth[0];
+            win[0] = hit ? tslot : win[0];
+            bw0[0] = hit ? a0 : bw0[0];
+            bw1[0] = hit ? a1 : bw1[0];
+            bw2[0] = hit ? a2 : bw2[0];
         }
         wave_sync();                                                        // before the next group's fill
     }
@@ -1103,7 +1104,6 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
     // k_geometry) or the launch order; either way a permutation of the bins, so the pixels do not
     // depend on it
     const uint32_t bid = order ? order[blockIdx.x] : blockIdx.x;
-    if (S3R_ORDER_WALL && order && threadIdx.x == 0) sh.t_start = (uint32_t)wall_clock64();   // in LDS: no live registers
     const uint32_t blk = bid / segs, seg = bid - blk * segs;
     const uint32_t nst = start_entries_of(W);
     auto row_of = [&](uint32_t lr) { return ((lr / band) * nparts + part) * band + lr % band; };
@@ -1163,7 +1163,7 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         }
         S3R_WGT(3);
         if (order && threadIdx.x == 0)
-            order[gridDim.x + bid] = S3R_ORDER_WALL ? (uint32_t)wall_clock64() - sh.t_start : kWorkSky;
+            order[gridDim.x + bid] = kWorkSky;
         return;
     }
     if (npairs > kPairMax) {
@@ -1416,20 +1416,16 @@ __global__ void __launch_bounds__(64 * kWaves, WF ? S3R_OCC_WIDE : S3R_OCC) k_fr
         }
     }
     S3R_WGT(3);
-    // this bin's cost for the buffer set's next order_bins: its waves' work units (S3R_ORDER_WALL:
-    // wave 0's wall time, 10 ns ticks)
+    // this bin's cost for the buffer set's next order_bins: its waves' work units (the bins' measured
+    // wall times, rounds 3-4, were retired in round 6: see kWorkFill)
     if (order) {
-        if (S3R_ORDER_WALL) {
-            if (threadIdx.x == 0) order[gridDim.x + bid] = (uint32_t)wall_clock64() - sh.t_start;
-        } else {
-            if (lane == 0) sh.wwork[wave] = wk;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                uint32_t c = 0;
+        if (lane == 0) sh.wwork[wave] = wk;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t c = 0;
 #pragma unroll
-                for (uint32_t w = 0; w < kWaves; w++) c += sh.wwork[w];
-                order[gridDim.x + bid] = c;
-            }
+            for (uint32_t w = 0; w < kWaves; w++) c += sh.wwork[w];
+            order[gridDim.x + bid] = c;
         }
     }
     S3R_WGC_STORE(n0);
@@ -1504,12 +1500,11 @@ struct alignas(16) RasterRec {
 };
 static_assert(sizeof(RasterRec) == 48, "RasterRec layout");
 
-// A bin / list entry is a slot, | kNoRecBit when the slot has no raster record.  With NOREC
-// (k_tile_setup; delivered frames) the setup writes no record for a slot the raster can set up again
-// from the scene -- an original triangle wholly past the near plane -- and marks its entry; the
-// recomputing raster (k_tile_raster<STAGE, true>, resolve_pixel<DEFER, true>) rebuilds its box, bound,
-// 1/z and steps from its corners (the same operations on the same operands: the same floats).  The
-// clip's slots always keep their records.
+// A bin / list entry is a slot, | kNoRecBit when the slot has no raster record.  k_tile_setup writes
+// no record for a slot the raster can set up again from the scene -- an original triangle wholly past
+// the near plane -- and marks its entry; the raster (k_tile_raster, resolve_pixel<DEFER, true>)
+// rebuilds its box, bound, 1/z and steps from its corners (the same operations on the same operands:
+// the same floats).  The clip's slots (k_tile_clip) keep their records.
 constexpr uint32_t kNoRecBit = 0x80000000u;
 
 // The corner's camera-space and raster position (render.cpp:286, :288).  The two projections share
@@ -1851,7 +1846,7 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
                                           uint32_t *__restrict__ counts, uint32_t *__restrict__ tbin = nullptr,
                                           uint32_t bin_cap = 0, uint32_t *__restrict__ ovf = nullptr, bool rec = true) {
     uint32_t bx = kDeadBox, by = 0;
-    const bool keep = rec;                              // (norec frames: only the clip's slots keep records)
+    const bool keep = rec;                              // (only the clip's slots keep records)
     TileSpan sp{0, 1, 0, 0, 0};
     if (live) {
         // the span first (it does not depend on the depth bucket) and the corners stored before the
@@ -1894,10 +1889,10 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
 // setup is memory-latency-bound).
 // (occupancy caps of 7 / 8 waves per SIMD, 72 / 64 VGPRs, measured slower: 580 -> 605 / 845 us, part 0
 // of 8 129 -> 171 / 218 us; profiles/r05_setup_occ_ab.txt)
-// (the record-writing instances take 85-87 VGPRs, occupancy 5, since the NOREC ones joined them;
-// capped at 80 -- occupancy 6, 12-20 B spilled -- the pipelined stress frame lost 3 %, part 0 of 8
-// 6 %: profiles/r05_rec0_ab.txt)
-template <bool VS, bool CL, bool NOREC>
+// No raster record for the triangles set up here (the raster rebuilds them from the corners,
+// kNoRecBit): round 5 measured the record-writing setup slower on every frame kind (stress scene,
+// profiles/r05_rec0_ab.txt: setup 548-554 -> 434 us, 1.34 -> 0.84 GB per frame) and round 6 retired it.
+template <bool VS, bool CL>
 __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ vtx, const uint32_t *__restrict__ vidx,
                                                     uint32_t ntri, const uint32_t *__restrict__ cmap,
                                                     const uint32_t *__restrict__ cperm,
@@ -1922,7 +1917,8 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     // cull's position for the iteration after that -- an iteration's loads are in flight while the
     // iteration before sets up and bins its triangles, so a wave waits on no load chain
     const uint32_t step = per * 256u, jl = rank * 256u + threadIdx.x;
-    auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : b0 + jj; };
+    // (without clusters cperm, when given, is the whole frame's processing order: position -> slot)
+    auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : (cperm ? cperm[b0 + jj] : b0 + jj); };
     const float4 *__restrict__ src = VS ? vrv : vtx;
     uint32_t t_cur = 0, t_nxt = 0, vi_nxt[3] = {0, 0, 0}, q_next = 0;
     float4 c_cur[3] = {make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0)};
@@ -1969,7 +1965,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
         emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4,
-                  !NOREC);
+                  false);
     }
 }
 
@@ -2002,10 +1998,8 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
         uint32_t t = 0;
         if (j < n) {
             t = clipq[b0 + j];
-            if (CL) {
-                t = cmap[t];
-                if (cperm) t = cperm[t];
-            }
+            if (CL) t = cmap[t];
+            if (cperm) t = cperm[t];
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
@@ -2255,7 +2249,7 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
 // winner needs a full setup go to the deferred queue (k_tile_resolve_deferred).  (Round 4 measured
 // the split form -- keys through HBM, a per-pixel resolve launch -- slower everywhere: stress scene
 // whole frame 800 -> 854 fps fused, delivered 583 -> 614, part 0 of 8 4 491 -> 4 672; it is gone.)
-template <uint32_t STAGE = kTileStage, bool RC = false>
+template <uint32_t STAGE = kTileStage>
 #ifndef S3R_TOCC
 #define S3R_TOCC 6                     // min waves per SIMD of the fused raster: 80 VGPRs (92 uncapped, occupancy 5);
 #endif                                 // the 256-stage instance stays at 4 (its LDS).  Stress scene, one box
@@ -2319,11 +2313,11 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
     }
     // software pipeline: stage c0 + STAGE's list entries and records are loaded into registers
     // while stage c0's items run
-    uint32_t s_nx = 0, b_nx = 0;                 // (b_nx: the entry's depth bucket, RC)
+    uint32_t s_nx = 0, b_nx = 0;                 // (b_nx: the entry's depth bucket)
     float4 q0n = make_float4(0, 0, 0, 0), q1n = q0n, q2n = q0n;
     auto fetch = [&](uint32_t c) {
         if (tid < STAGE && c + tid < n) {
-            if (RC) {                                    // the entry's depth bucket (its bound's ceiling)
+            {                                            // the entry's depth bucket (its bound's ceiling)
                 uint32_t bb = 0;
 #pragma unroll
                 for (uint32_t step = 16; step >= 1u; step >>= 1)
@@ -2353,7 +2347,7 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
                 s_nx = 0;
             }
 #endif
-            if (RC && (s_nx & kNoRecBit)) {                 // no record: the corners (set up at staging)
+            if (s_nx & kNoRecBit) {                 // no record: the corners (set up at staging)
                 const uint32_t *vi = sc.vidx + 3ull * (s_nx & ~kNoRecBit);
                 const uint32_t v0 = vi[0], v1 = vi[1], v2 = vi[2];
                 q0n = sc.vtx[v0]; q1n = sc.vtx[v1]; q2n = sc.vtx[v2];
@@ -2405,9 +2399,9 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
         const uint32_t j = c0 + tid;
         uint32_t nr = 0;
         if (tid < STAGE && j < n) {
-            const uint32_t s = RC ? s_nx & ~kNoRecBit : s_nx;
+            const uint32_t s = s_nx & ~kNoRecBit;
             float4 q0 = q0n, q1 = q1n, q2 = q2n;
-            if (RC && (s_nx & kNoRecBit)) {
+            if (s_nx & kNoRecBit) {
                 // the record k_tile_setup would have written, from the corners: box, bound, 1/z, corners
                 Vert d[3];
                 const float4 cc[3] = {q0, q1, q2};
@@ -2563,7 +2557,7 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
             const unsigned long long k = in ? ls.key[rr * kKeyStride + cc] : 0ull;
             const uint32_t y = row_of(lr);
             uint32_t v = kBackground;
-            if (in) v = resolve_pixel<true, RC>(sc, k, x, y);
+            if (in) v = resolve_pixel<true, true>(sc, k, x, y);
             const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
 #ifdef S3R_BOUNDS
             if (in && idx >= (size_t)W * (frame_rows ? (uint32_t)sc.sh : rows_local)) {
@@ -3061,13 +3055,13 @@ template <class K> uint32_t shard_grid(K *kernel, uint64_t work, uint32_t dflt =
     return shard_grid(reinterpret_cast<const void *>(kernel), work, dflt);
 }
 
-template <bool VS, bool CL, bool NOREC>
-void setup_launch_nr(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
+template <bool VS, bool CL>
+void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
                   float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
                   void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
-                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap) {
-    const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
-    { hipLaunchKernelGGL((k_tile_setup<VS, CL, NOREC>), dim3(shard_grid(k_tile_setup<VS, CL, NOREC>, ntri, CL ? 256 : 1024)), dim3(256),
+                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap, const uint32_t *sperm = nullptr) {
+    const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : sperm, *tab = CL ? cl->shard : nullptr;
+    { hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
                        0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, xoff,
                        (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap); after_launch("k_tile_setup", st); }
     // the clip queue is short (triangles crossing the near plane): one workgroup per shard
@@ -3075,25 +3069,13 @@ void setup_launch_nr(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, con
                        factor, sw, sh, band, nparts, part, tx, xoff, (RasterRec *)recs, live, clipq, ctr, counts, tbin,
                        bin_cap); after_launch("k_tile_clip", st); }
 }
-template <bool VS, bool CL>
-void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
-                  float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
-                  void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
-                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap, bool norec) {
-    if (norec)
-        setup_launch_nr<VS, CL, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                      ctr, counts, vrv, st, tbin, bin_cap);
-    else
-        setup_launch_nr<VS, CL, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                       ctr, counts, vrv, st, tbin, bin_cap);
-}
 
 void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const Mat34 &m, float factor, float sw,
                        float sh, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part, uint32_t rows_local,
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
                        uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag, uint32_t *tbin,
-                       uint32_t bin_cap, uint32_t xoff, bool norec) {
+                       uint32_t bin_cap, uint32_t xoff, const uint32_t *sperm) {
     const uint64_t ns = tile_slots(W, rows_local, xoff);  // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
@@ -3104,13 +3086,13 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
             { hipLaunchKernelGGL(k_cluster_cull, dim3((cl->ncl + 255) / 256), dim3(256), 0, st, cl->sphere, cl->first,
                                cl->ncl, cl->shard, m, factor, sw, sh, band, nparts, part, cl->cmap, ctr); after_launch("k_cluster_cull", st); }
             setup_launch<false, true>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                      ctr, counts, nullptr, st, tbin, bin_cap, norec);
+                                      ctr, counts, nullptr, st, tbin, bin_cap);
         } else if (vrv) {
             setup_launch<true, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live, clipq,
-                                      ctr, counts, vrv, st, tbin, bin_cap, norec);
+                                      ctr, counts, vrv, st, tbin, bin_cap);
         } else {
             setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live,
-                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap, norec);
+                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap, sperm);
         }
     }
     if (bin_cap) {                                       // bins mode: binned already
@@ -3148,27 +3130,23 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t *out, uint32_t W, uint32_t band, uint32_t nparts, uint32_t part,
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows, uint32_t *counts,
-                                uint32_t bin_cap, uint32_t xoff, uint32_t *sum_host, bool norec) {
+                                uint32_t bin_cap, uint32_t xoff, uint32_t *sum_host) {
     const uint32_t tx = tile_grid_x(W, xoff), ty = (rows_local + kTileH - 1) / kTileH;
     if (tx == 0 || ty == 0) return;
     const ShadeScene sc{(const RasterRec *)recs, vtx, nrm, pay, disc, vidx, aidx, tex, ntri, ntex, m, factor, sw, sh};
     // frames written into the caller's buffer stage 256 triangles at a time, frames into HBM 128: on
     // the stress scene (one MI355X, profiles/r04_tstage_ab.txt) the wider stage delivers 772 / 726 ->
     // 802 / 803 fps (the raster waits on the link anyway, and half the stage rounds and barriers
-    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy).  norec frames take
-    // the recomputing instances (the records the setup left out rebuilt at staging, kNoRecBit)
+    // remain), but costs the HBM frame 975 -> 952 fps (its LDS lowers the occupancy).  Both rebuild the
+    // records the setup leaves out at staging (kNoRecBit).
     const uint32_t capw = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
-    if (!frame_rows && norec)
-        { hipLaunchKernelGGL((k_tile_raster<kTileStage, true>), dim3(tx * ty), dim3(kTileThreads), 0, st,
-                           (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list, capw, sc,
-                           out, 0u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
-    else if (frame_rows) {
-        hipLaunchKernelGGL((k_tile_raster<kTileStageLink, true>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+    if (frame_rows)
+        { hipLaunchKernelGGL((k_tile_raster<kTileStageLink>), dim3(tx * ty), dim3(kTileThreads), 0, st,
                            (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list,
                            capw, sc, out, 1u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
     else
-        { hipLaunchKernelGGL((k_tile_raster<>), dim3(tx * ty), dim3(kTileThreads), 0, st, (const RasterRec *)recs, W,
-                           band, nparts, part, rows_local, tx, offs, ctr, list, capw, sc,
+        { hipLaunchKernelGGL((k_tile_raster<kTileStage>), dim3(tx * ty), dim3(kTileThreads), 0, st,
+                           (const RasterRec *)recs, W, band, nparts, part, rows_local, tx, offs, ctr, list, capw, sc,
                            out, 0u, deferred, counts, bin_cap, xoff); after_launch("k_tile_raster", st); }
     { hipLaunchKernelGGL(k_tile_resolve_deferred, dim3(64), dim3(256), 0, st, sc, (const uint4 *)deferred, ctr, out,
                        bin_cap ? 1u : 0u, sum_host); after_launch("k_tile_resolve_deferred", st); }

@@ -43,6 +43,8 @@
 namespace s3r_host {   // clusters.cpp
 void build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_t ntri, uint32_t kmin, uint32_t kmax,
                     std::vector<uint32_t> &first, std::vector<float> &sphere, std::vector<uint32_t> &perm);
+void spatial_order(const std::vector<uint32_t> &first, const std::vector<float> &sphere, const std::vector<uint32_t> &perm,
+                   uint32_t ntri, std::vector<uint32_t> &out);
 }
 namespace s3r_host {   // host_fill.cpp
 void fill_words(uint32_t *p, size_t n, uint32_t v);
@@ -241,6 +243,9 @@ constexpr uint64_t kNearCheckMaxTri = 1024;   // the host's near-plane check: sc
 constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
 constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set
 constexpr int kMaxDevices = 64;
+#ifndef S3R_SPATIAL
+#define S3R_SPATIAL 1               // whole tile-path frames set triangles up in the clusters' Morton order
+#endif
 
 // S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
 struct HostProf {
@@ -287,7 +292,7 @@ struct Dev {
     uint32_t *tile_list[kSets] = {};
     void *scan_temp = nullptr;                 // rocprim scan of the (tile, bucket) counts
     size_t scan_temp_bytes = 0;
-    float4 *vrv = nullptr;                     // tile path vertex stage (S3R_VERTEX_STAGE): projected vertices
+    float4 *vrv = nullptr;                     // tile path vertex stage (frame parts): projected vertices
     void *recs[kSets] = {};        // 2T raster records (positions-only setup)
     uint4 *live[kSets] = {};       // 2T live entries (tile box, rows, slot), per shard
     uint32_t *clipq = nullptr;     // T: positions whose triangle crosses the near plane (one: setups run on geo[0])
@@ -296,6 +301,7 @@ struct Dev {
     // and the cull's per-frame position list (one: every tile-path setup runs on geo[0])
     float4 *cl_sphere = nullptr;
     uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_shard = nullptr, *cl_map = nullptr;
+    uint32_t *sp_perm = nullptr;     // whole-frame setup order: the clusters in Morton order (clusters.cpp spatial_order)
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
     size_t deferred_cap = 0;
@@ -315,7 +321,6 @@ struct Dev {
     uint32_t tile_pending_set = 0, tile_W = 0, tile_H = 0, tile_band = 0, tile_nparts = 1, tile_part = 0, tile_rows = 0;
     uint32_t *tile_out = nullptr;
     bool tile_frame_rows = false;
-    bool tile_norec = false;                   // the tile frame's setup writes records for the clip's slots only
     uint64_t tile_overflows = 0, tile_readbacks = 0;
     uint64_t last_pairs = 0;                   // tile path: (slot, tile) pairs of the last frame
     int last_set = -1;                         // tile path: the last frame's buffer set (refresh_pairs)
@@ -364,6 +369,7 @@ struct HostScene {
     std::vector<uint8_t> disc;
     std::vector<uint32_t> vidx, aidx, tex;
     std::vector<uint32_t> cl_first, cl_perm;   // clusters (tile path): position ranges, position -> slot
+    std::vector<uint32_t> sp_perm;             // whole-frame setup order (spatial_order)
     std::vector<uint32_t> cl_shard;            // where each shard's positions start (cluster_shard_table)
     std::vector<float> cl_sphere;              // 4 per cluster: centre, radius
 };
@@ -551,7 +557,6 @@ struct Lib {
     uintptr_t unmapped_a = 0;
     uint64_t unmapped_epoch = 0;
     // environment switches read once per library state (release_all resets them: a configure re-reads)
-    int env_row_starts = -1, env_host_uncached = -1, env_slot_cull = -1, env_tile_norec = -1;
     // fill-thread placement: frames in a row whose buffer sat on another node than the placement's
     int fill_node_streak = 0;
     uint64_t link_bytes = 0;                   // bytes the devices sent over their links, last frame
@@ -562,16 +567,6 @@ struct Lib {
 };
 
 Lib g;
-
-// A default-on switch from the environment (unset or non-zero: on), cached in `slot` until the
-// library state is reset (s3r_configure / s3r_shutdown).
-bool env_on(int &slot, const char *name) {
-    if (slot < 0) {
-        const char *e = getenv(name);
-        slot = !e || atoi(e) != 0 ? 1 : 0;
-    }
-    return slot == 1;
-}
 
 float config_scale() {
     const float fov = (float)M_PI / 5.f;        // render.cpp:91
@@ -714,6 +709,7 @@ HostScene read_scene() {
                                  (uint32_t)ntri, 8, 32, s.cl_first, s.cl_sphere, s.cl_perm);
     g.ncl = s.cl_first.empty() ? 0 : (uint32_t)s.cl_first.size() - 1;
     if (g.ncl) s.cl_shard = cluster_shard_table(s.cl_first);
+    if (g.ncl && S3R_SPATIAL) s3r_host::spatial_order(s.cl_first, s.cl_sphere, s.cl_perm, (uint32_t)ntri, s.sp_perm);
     return s;
 }
 
@@ -762,6 +758,10 @@ void dev_init(Dev &d, const HostScene &s) {
         HIPCHECK(hipMemcpy(d.cl_shard, s.cl_shard.data(), (kTileShards + 1) * 4, hipMemcpyHostToDevice));
         HIPCHECK(hipMemcpy(d.cl_sphere, s.cl_sphere.data(), (size_t)g.ncl * 16, hipMemcpyHostToDevice));
         HIPCHECK(hipMemcpy(d.cl_first, s.cl_first.data(), ((size_t)g.ncl + 1) * 4, hipMemcpyHostToDevice));
+        if (!s.sp_perm.empty()) {
+            d.sp_perm = dalloc<uint32_t>(ntri);
+            HIPCHECK(hipMemcpy(d.sp_perm, s.sp_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
+        }
         if (!s.cl_perm.empty()) {
             d.cl_perm = dalloc<uint32_t>(ntri);
             HIPCHECK(hipMemcpy(d.cl_perm, s.cl_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
@@ -845,7 +845,7 @@ void unregister_all() {
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
-                    d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
+                    d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq, d.sp_perm};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases tile_ctr
@@ -941,7 +941,7 @@ void frame_begin(const Input *input, uint32_t width, uint32_t height) {
     if (k.valid && k.factor == g.factor && k.W == width && k.H == height && !memcmp(&k.m, &g.m, sizeof(Mat34))) return;
     g.clip_slots = near_plane_crossing();
     g.live.on = 0;
-    if (!g.clip_slots && env_on(g.env_slot_cull, "S3R_SLOT_CULL")) cull_slots(width, height);
+    if (!g.clip_slots) cull_slots(width, height);
     k = Lib::CullKey{g.m, g.factor, width, height, true};
 }
 
@@ -1183,7 +1183,7 @@ void tile_fragment_stage(Dev &d, uint32_t p, uint32_t W, uint32_t band, uint32_t
     launch_tile_raster_resolve(d.recs[p], d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, g.ntri, g.m, g.factor, sw, sh,
                                d.tex, g.ntex, out, W, band, nparts, part, rows_local, d.tile_offs[p], d.tile_ctr[p],
                                list, d.tile_list_cap[p], d.deferred, st, frame_rows, bcounts, bcap, d.tile_xoff,
-                               d.tile_sum_dev + kSumWords * p, d.tile_norec);
+                               d.tile_sum_dev + kSumWords * p);
     if (ts) HIPCHECK(hipEventRecord(ts->frag1, st));
     HIPCHECK(hipEventRecord(d.frag_done[p], st));
     HIPCHECK(hipGetLastError());
@@ -1355,7 +1355,7 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
                           d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p],
                           d.tile_cursor[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl,
                           d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u,
-                          d.tile_xoff, d.tile_norec);
+                          d.tile_xoff, d.sp_perm);
         wait_tile_summary(d, p, geo);
         if (!bins) {
             grow_tile_list(d, p, sum[2]);
@@ -1397,10 +1397,8 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     }
     // vertex stage (k_tile_vertex): measured on the 20 M-triangle stress scene at 4K, part 0 of 8
     // 1 996 -> 2 108 fps (setup 307 -> 235 us + 57 us for the stage), whole frame 826 -> 808 fps: on
-    // for frame parts, where the per-triangle setup is replicated on every device; S3R_VERTEX_STAGE
-    // = 0 / 1 forces it
-    const char *vs_env = getenv("S3R_VERTEX_STAGE");
-    if (vs_env ? atoi(vs_env) != 0 : nparts > 1 && !tile_clusters(d, nparts).ncl) {
+    // for frame parts without clusters, where the per-triangle setup is replicated on every device
+    if (nparts > 1 && !tile_clusters(d, nparts).ncl) {
         if (!d.vrv) d.vrv = dalloc<float4>(g.nv);
     } else if (d.vrv) {
         sync_device("tile path: dropping the vertex stage", d.device, d.frame_no);
@@ -1430,22 +1428,15 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     if (bins_on(d)) ensure_bins(d, nt);
     const bool bins = bins_on(d);
     if (!bins) ensure_live(d);
-    // no raster records for the slots the raster can set up again (kernels.hip kNoRecBit; the
-    // fragment stage is then the recomputing raster).  Stress scene, one MI355X
-    // (profiles/r05_rec0_ab.txt): setup 548-554 -> 434 us, its traffic 1.34 -> 0.84 GB; delivered
-    // frames 831-833 -> 915-924 fps; frames into HBM (the raster 423 -> 498 us) 1 151 -> 1 174 fps
-    // whole, part 0 of 8 at the 135-row band 6 503-6 524 -> 6 846-6 880.  S3R_TILE_NOREC=0: records for
-    // every frame, 2: for frames into HBM only.
-    if (g.env_tile_norec < 0) {
-        const char *e = getenv("S3R_TILE_NOREC");
-        g.env_tile_norec = e ? atoi(e) : 1;
-    }
-    d.tile_norec = g.env_tile_norec == 1 || (frame_rows && g.env_tile_norec == 2);
+    // no raster records for the slots the raster can set up again (kernels.hip kNoRecBit).  Stress
+    // scene, one MI355X (profiles/r05_rec0_ab.txt): setup 548-554 -> 434 us, its traffic 1.34 -> 0.84 GB;
+    // delivered frames 831-833 -> 915-924 fps; frames into HBM 1 151 -> 1 174 fps whole, part 0 of 8 at
+    // the 135-row band 6 503-6 524 -> 6 846-6 880 (the record-writing setup was retired in round 6)
     if (test_hold_ms() && d.frame_no >= 2) launch_test_hold(test_hold_ms(), geo);
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff, d.tile_norec);
+                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff, d.sp_perm);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are
@@ -1586,8 +1577,8 @@ void render_core(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts,
     // host fill: the geometry launch also publishes the bins' sky flags, as soon as every workgroup's
     // pair reservations are in (one extra workgroup waits for them on per-row-block counters)
     // delivered frames: the geometry tabulates row starts only, the fragment workgroups walk along
-    // their rows themselves (kernels.hip k_geometry); S3R_ROW_STARTS=0: the full start table
-    const bool row_starts = hf != nullptr && env_on(g.env_row_starts, "S3R_ROW_STARTS");
+    // their rows themselves (kernels.hip k_geometry)
+    const bool row_starts = hf != nullptr;
     GeoSkyFlags gsf{};
     if (hf && hf->flags_dev) {
         if (!d.geo_cnt) {
@@ -1675,10 +1666,9 @@ bool host_pinned(void *p, size_t n) {
     // mapped: the host-fill delivery has the GPU write covered bins straight into these pages;
     // uncached (the extended fine-grained pool): with the fragment kernel's line-grid stores the
     // link then carries whole 64-B lines (54.0 vs 52.0 GB/s for a malloc + 16-B buffer,
-    // tools/micro/pcie_write.hip); S3R_HOST_UNCACHED=0 registers it as before.  A runtime that
-    // refuses the flag gets the plain registration.
-    bool ok = env_on(g.env_host_uncached, "S3R_HOST_UNCACHED") && hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped |
-                                                                hipExtHostRegisterUncached) == hipSuccess;
+    // tools/micro/pcie_write.hip).  A runtime that refuses the flag gets the plain registration.
+    bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped |
+                              hipExtHostRegisterUncached) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         ok = hipHostRegister((void *)a, b - a, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;

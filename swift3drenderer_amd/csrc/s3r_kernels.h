@@ -167,9 +167,11 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st,
                        float4 *vrv = nullptr, uint32_t nv = 0, const TileClusters *cl = nullptr,
                        uint32_t *sum_host = nullptr, uint32_t tag = 0, uint32_t *tbin = nullptr, uint32_t bin_cap = 0,
-                       uint32_t xoff = 0, bool norec = false);
-// norec: no raster record for the slots the raster can set up again from the scene (kernels.hip
-// kNoRecBit) -- the frame's launch_tile_raster_resolve must then be given norec too.
+                       uint32_t xoff = 0, const uint32_t *sperm = nullptr);
+// No raster record is written for the slots the raster can set up again from the scene (kernels.hip
+// kNoRecBit); the clip's slots keep theirs.  sperm (may be null; used without clusters and without the
+// vertex stage): the setup's processing order, position -> slot (render_api.cpp sp_perm) -- any
+// permutation gives the same pixels.
 // tbin / bin_cap (bins mode): every (tile, bucket) slot s gets bin_cap entries at tbin + s x bin_cap
 // and counts[s] of them filled by the setup itself -- no scan, no fill pass; the summary's word 4 is
 // then the count the fullest slot needed when it exceeded bin_cap (0: none; the frame is rendered
@@ -194,8 +196,7 @@ void launch_tile_raster_resolve(const void *recs, const float4 *vtx, const float
                                 uint32_t rows_local, const uint32_t *offs, uint32_t *ctr, const uint32_t *list,
                                 uint64_t cap, uint4 *deferred, hipStream_t st, bool frame_rows,
                                 uint32_t *counts = nullptr, uint32_t bin_cap = 0, uint32_t xoff = 0,
-                                uint32_t *sum_host = nullptr,       // bins: the entries' total (launch_tile_resolve_deferred)
-                                bool norec = false);                // the setup ran with norec: the recomputing raster
+                                uint32_t *sum_host = nullptr);      // bins: the entries' total (launch_tile_resolve_deferred)
 // Those pixels, shaded with the winner's full setup (after every resolve launch of the frame).
 void launch_tile_resolve_deferred(const void *recs, const float4 *vtx, const float4 *nrm, const float4 *pay,
                                   const uint8_t *disc, const uint32_t *vidx, const uint32_t *aidx, uint32_t ntri,

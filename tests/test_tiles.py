@@ -271,34 +271,6 @@ def test_tile_bands_reassemble(gpu_renderer, icosa_dir, band, nparts):
     assert np.array_equal(got, full), diff(got, full)
 
 
-@pytest.mark.parametrize('norec', ['0', '1', '2'])
-def test_record_modes_match_oracle(gpu_renderer, icosa_dir, scene_dir, monkeypatch, norec):
-    """The tile setup's raster records: none for the slots the raster rebuilds (S3R_TILE_NOREC=1, the
-    default: kernels.hip kNoRecBit, the recomputing raster and resolve), records for every slot (0), or
-    for frames into HBM only (2) -- delivered frames and a device-resident whole frame, on the stress
-    scene and on the packaged scene crossing the near plane (clip slots keep their records in every
-    mode), each against the oracle."""
-    import torch
-    monkeypatch.setenv('S3R_TILE_NOREC', norec)
-    r = gpu_renderer
-    for path, pose, (w, h) in [(icosa_dir[2000], 'P_id', (1280, 720)), (scene_dir['full'], 'P_clip', (640, 480))]:
-        r.configure(path)                              # (the library re-reads its environment)
-        r.set_raster_path('tiles')
-        try:
-            script = poses.script(pose)
-            want = oracle_render_pose(path, script, w, h, extra_frames=1)
-            got = render_pose(r, path, script, w, h, extra_frames=1)
-            assert np.array_equal(got, want), f'{pose} delivered: ' + diff(got, want)
-            buf = torch.empty((h, w), dtype=torch.int32, device='cuda')
-            hold = (0, 0, 0, 0) + tuple(script[-1][4:6])
-            r.render_bands(hold, w, h, h, 1, 0, buf.data_ptr(), 0)
-            torch.cuda.synchronize()
-            dev = buf.cpu().numpy().view(np.uint32)
-            assert np.array_equal(dev, want), f'{pose} in HBM: ' + diff(dev, want)
-        finally:
-            r.set_raster_path('auto')
-
-
 def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
     """Row path and tile path give the same 4K frame (both are exact)."""
     path = scene_dir['full']
@@ -316,21 +288,34 @@ def test_paths_agree_on_packaged_4k(gpu_renderer, scene_dir):
 @pytest.mark.parametrize('case', [('full', 'P_clip', 640, 480), ('full', 'P_over', 1000, 333), ('stress', 'P_id', 1920, 1080),
                                   ('stress', 'P_strafe', 1280, 720)])
 def test_vertex_stage_matches_oracle(gpu_renderer, scene_dir, icosa_dir, monkeypatch, case):
-    """The tile path with the vertex stage (S3R_VERTEX_STAGE=1: every vertex projected once by
-    k_tile_vertex, triangles set up from those; the near-plane clip recomputes its corners) -- the
-    setup without clusters (S3R_CLUSTERS=0), where the vertex stage applies."""
-    monkeypatch.setenv('S3R_VERTEX_STAGE', '1')
+    """The tile path's vertex stage (every vertex projected once by k_tile_vertex, triangles set up
+    from those; the near-plane clip recomputes its corners): the library runs it for frame parts of a
+    scene without clusters (S3R_CLUSTERS=0 here), so the frame is rendered as 2 and 3 parts and
+    reassembled against the oracle."""
+    import torch
+    from swift3drenderer_amd.multi import assemble
     monkeypatch.setenv('S3R_CLUSTERS', '0')
     name, pose, w, h = case
     path = icosa_dir[2000] if name == 'stress' else scene_dir[name]
-    gpu_renderer.set_raster_path('tiles')
+    r = gpu_renderer
+    r.set_raster_path('tiles')
     try:
         script = poses.script(pose)
         want = oracle_render_pose(path, script, w, h, extra_frames=1)
-        got = render_pose(gpu_renderer, path, script, w, h, extra_frames=1)
-        assert np.array_equal(got, want), diff(got, want)
+        render_pose(r, path, script, w, h)              # (the camera at the pose; the library re-reads its env)
+        hold = (0, 0, 0, 0) + tuple(script[-1][4:6])
+        for nparts, band in ((2, 16), (3, 7)):
+            parts = []
+            for part in range(nparts):
+                rows = r.lib.s3r_band_rows_local(h, band, nparts, part)
+                buf = torch.empty((max(rows, 1), w), dtype=torch.int32, device='cuda')
+                r.render_bands(hold, w, h, band, nparts, part, buf.data_ptr(), 0)
+                torch.cuda.synchronize()
+                parts.append(buf[:rows].cpu().numpy().view(np.uint32))
+            got = assemble(parts, h, band)
+            assert np.array_equal(got, want), f'{nparts} parts: ' + diff(got, want)
     finally:
-        gpu_renderer.set_raster_path('auto')
+        r.set_raster_path('auto')
 
 
 def test_sync_frames_without_list_readback(gpu_renderer, icosa_dir, monkeypatch):

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/par.log 2>&1 || { echo PARITY_FAIL; tail -30 gpurun_out/par.log; exit 1; }
 tail -1 gpurun_out/par.log
 for pose in P_over P_id P_clip; do
-  timeout -k 10 120 python bench.py --pose $pose --steps 200 --warmup 20 --no-cpu-baseline $BENCH_EXTRA 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$pose', d['value'], 'fps frag_ms', d['fragment_kernel_ms'], 'frac', d['roofline']['frac'])" || exit 1
+  timeout -k 10 120 python bench.py --pose $pose --steps 200 --warmup 20 --no-cpu-baseline $BENCH_EXTRA 2>>gpurun_out/tools_stderr.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$pose', d['value'], 'fps frag_ms', d['fragment_kernel_ms'], 'frac', d['roofline']['frac'])" || exit 1
 done
 export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/pq -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline $BENCH_EXTRA > gpurun_out/pq.log 2>&1 || exit 1

@@ -77,12 +77,83 @@ for recipe in "$@"; do
       lds_pmc tabpad_pmc_pad || exit 1
       lds_pmc tabpad_pmc_pad0 S3R_LIB=build/librender_pad0.so || exit 1
       ;;
+    ab)   # product vs the variant library $AB (build/librender_$AB.so): bench x2, part 0 of 8, rocprof, counters
+      V=build/librender_$AB.so
+      for i in 1 2; do
+        bench_line ${AB}_bench_prod$i || exit 1
+        bench_line ${AB}_bench_var$i S3R_LIB=$V || exit 1
+      done
+      part8 ${AB}_part8_prod || exit 1
+      part8 ${AB}_part8_var S3R_LIB=$V || exit 1
+      kstats ${AB}_k_prod || exit 1
+      kstats ${AB}_k_var S3R_LIB=$V || exit 1
+      lds_pmc ${AB}_pmc_prod || exit 1
+      lds_pmc ${AB}_pmc_var S3R_LIB=$V || exit 1
+      ;;
+    k8)   # part 0 of 8 of the 8K frame (config 4's split) and of the 4K frame under fragment-launch thresholds
+      for sz in "7680 4320" "3840 2160"; do
+        set -- $sz
+        for envs in "S3R_NOTHING=0" "S3R_WATERFALL_BINS=2000" "S3R_LPT_MIN=100000000" "S3R_WATERFALL_BINS=2000 S3R_LPT_MIN=100000000"; do
+          tag=k8_${1}_$(echo $envs | tr ' =' '__')
+          step $tag 120 env $envs python3 -u tools/overhead_probe.py --width $1 --height $2 --nparts 8 --steps 2000 || exit 1
+          python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/$tag.log') if l.startswith('{')][-1]
+print('  $1 $envs: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 2), 'host_us', round(d['host_enqueue_us'], 2))"
+        done
+      done
+      ;;
+    spab)  # config 5 whole frame: the setup in the clusters' Morton order (product) vs file order (build S3R_SPATIAL=0)
+      [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
+      for v in prod sp0; do
+        L=""; [ $v = sp0 ] && L=build/librender_sp0.so
+        step spab_bench_$v 300 env ${L:+S3R_LIB=$L} python3 -u bench.py --scene icosa-stress --pose P_id --data $STRESS --no-cpu-baseline || exit 1
+        grep '^{' "$OUT/spab_bench_$v.log" | tail -1 > "$OUT/spab_bench_$v.json"
+        python3 -c "import json; d=json.load(open('$OUT/spab_bench_$v.json')); print('  $v stress', round(d['value']), 'fps  device', round(d['device_fps']), 'setup_ms', d['setup_ms'], 'frag_ms', d['fragment_kernel_ms'])"
+        step spab_k_$v 300 env ${L:+S3R_LIB=$L} S3R_SERIAL=1 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/spab_k_$v" -o run -- \
+            python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $STRESS --steps 20 || exit 1
+        f=$(find "$OUT/spab_k_$v" -name '*kernel_stats.csv' | sort | tail -1)
+        python3 -c "
+import csv
+for r in list(csv.DictReader(open('$f')))[:6]: print('  $v %-50s %6s calls avg %9.1f us' % (r['Name'][:50], r['Calls'], float(r['AverageNs'])/1e3))"
+        for c in FETCH_SIZE WRITE_SIZE; do
+          step spab_pmc_${v}_$c 200 env ${L:+S3R_LIB=$L} rocprofv3 --pmc $c --output-format csv -d "$OUT/spab_pmc_$v/$c" -o run -- \
+              python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $STRESS --steps 10 || exit 1
+        done
+        python3 tools/pmc_summary.py "$OUT/spab_pmc_$v" --last 10 > "$OUT/spab_pmc_$v.txt" 2>&1 || exit 1
+        python3 -c "
+import json
+for k, c in json.load(open('$OUT/spab_pmc_$v/pmc_summary.json')).items():
+    if 'k_tile' in k: print('  $v %-44s FETCH %.1f MB  WRITE %.1f MB' % (k[-44:], c.get('FETCH_SIZE', 0) / 1024, c.get('WRITE_SIZE', 0) / 1024))"
+      done
+      ;;
     rowparity)   # the row path's parity suite
       step rowparity 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
           tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
       ;;
     stall)   # the bounded-wait tests (each a child process that must end with status 86)
       step stall 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_stall.py || exit 1
+      ;;
+    tiles)   # the tile path's parity suite
+      step tiles 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_tiles.py || exit 1
+      ;;
+    stress)  # config 5 (1 M icosahedra, 4K, tile path): the bench line, part 0 of 8 at the library's band
+      [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
+      step stress_bench 300 python3 -u bench.py --scene icosa-stress --pose P_id --data $STRESS --no-cpu-baseline || exit 1
+      grep '^{' "$OUT/stress_bench.log" | tail -1 > "$OUT/stress_bench.json"
+      python3 -c "import json; d=json.load(open('$OUT/stress_bench.json')); print('  stress', round(d['value']), 'fps  device', round(d['device_fps']), 'setup_ms', d['setup_ms'], 'frag_ms', d['fragment_kernel_ms'])"
+      step stress_part8 300 python3 -u tools/overhead_probe.py --scene icosa-stress --pose P_id --data $STRESS --nparts 8 --band 135 --steps 100 || exit 1
+      python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/stress_part8.log') if l.startswith('{')][-1]
+print('  stress part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 1))"
+      ;;
+    parts)   # every part of the N = 1, 2, 4, 8 band splits of configs 3, 4 (and 5 with PARTS_CONFIGS)
+      step parts 900 python3 -u tools/parts_all.py --configs ${PARTS_CONFIGS:-3,4} --out "$OUT/parts_all.jsonl" || exit 1
+      python3 -c "
+import json
+for l in open('$OUT/parts_all.jsonl'):
+    d=json.loads(l); print('  config', d['config'], 'N', d['N'], 'band', d['band'], 'slowest', d['slowest_us'], 'max/mean', d['max_over_mean'], 'eff', d['efficiency_per_gpu'])"
       ;;
     suite)   # the whole GPU suite, once
       step suite 1100 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests || exit 1

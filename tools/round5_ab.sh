@@ -71,6 +71,7 @@
 #                                                                   -> r05_slot_cull_ab.txt
 #   nearck    k_geometry without the clip-appended slots when the host's near-plane check allows it
 #             (product) vs always with them (noclipck build): parity, delivered frames, geometry timeline
+mkdir -p gpurun_out
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=${1:?recipe}
@@ -84,7 +85,7 @@ gpu_suite() {   # log, pytest args...
 }
 probe() {       # tag, env..., then overhead_probe args after --
   local tag=$1; shift; local envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
-  env "${envs[@]}" timeout -k 10 180 python3 tools/overhead_probe.py "$@" 2>/dev/null | grep '^{' | sed "s/^/$tag /" | cut -c1-200
+  env "${envs[@]}" timeout -k 10 180 python3 tools/overhead_probe.py "$@" 2>>gpurun_out/tools_stderr.log | grep '^{' | sed "s/^/$tag /" | cut -c1-200
 }
 
 case $R in
@@ -260,7 +261,7 @@ rec48)
       env S3R_SERIAL=1 ${lib:+S3R_LIB=$lib} timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d "$PWD/$OUT/pmc_${tag}_$c" -o run -- \
           python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $D --steps 10 > $OUT/pmc_${tag}_$c.log 2>&1 || { tail -5 $OUT/pmc_${tag}_$c.log; exit 1; }
     done
-    python3 tools/pmc_summary.py $OUT --last 10 > /dev/null 2>&1 || true
+    python3 tools/pmc_summary.py $OUT --last 10 >> gpurun_out/tools_output.log 2>&1 || true
     find $OUT -name '*kernel_trace.csv' -delete
   done
   for spec in rec64 rec48; do
