@@ -210,31 +210,6 @@ void build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_
     if (identity) std::vector<uint32_t>().swap(perm);
 }
 
-// The clusters' triangles in the Morton order of the clusters' centres (over the centres' box), as
-// position -> slot: the whole-frame tile setup's processing order (render_api.cpp).  Any order gives
-// the same pixels (the tile path's winner key carries the slot); a spatially coherent one keeps each
-// setup shard -- a contiguous range of positions, its workgroups on one XCD (kernels.hip shards) -- on
-// a compact part of the screen, so a (tile, bucket) bin's entries come from one XCD's L2 instead of
-// partial lines from all eight.
-void spatial_order(const std::vector<uint32_t> &first, const std::vector<float> &sphere, const std::vector<uint32_t> &perm,
-                   uint32_t ntri, std::vector<uint32_t> &out) {
-    out.clear();
-    const uint32_t ncl = first.empty() ? 0u : (uint32_t)first.size() - 1;
-    if (!ncl) return;
-    Box b;
-    for (uint32_t q = 0; q < ncl; q++)
-        if (std::isfinite(sphere[4 * q + 3])) b.add(&sphere[4 * q]);
-    std::vector<std::pair<uint64_t, uint32_t>> keyed(ncl);
-    for (uint32_t q = 0; q < ncl; q++) {
-        const double c[3] = {sphere[4 * q], sphere[4 * q + 1], sphere[4 * q + 2]};
-        keyed[q] = {std::isfinite(sphere[4 * q + 3]) ? morton(b, c) : ~0ull, q};
-    }
-    std::sort(keyed.begin(), keyed.end());
-    out.reserve(ntri);
-    for (const auto &kq : keyed)
-        for (uint32_t i = first[kq.second]; i < first[kq.second + 1]; i++) out.push_back(perm.empty() ? i : perm[i]);
-}
-
 }  // namespace s3r_host
 
 // Test hook (include/render.h s3r_build_clusters): the clusters of a vertex / index list, without a

@@ -1917,8 +1917,7 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     // cull's position for the iteration after that -- an iteration's loads are in flight while the
     // iteration before sets up and bins its triangles, so a wave waits on no load chain
     const uint32_t step = per * 256u, jl = rank * 256u + threadIdx.x;
-    // (without clusters cperm, when given, is the whole frame's processing order: position -> slot)
-    auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : (cperm ? cperm[b0 + jj] : b0 + jj); };
+    auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : b0 + jj; };
     const float4 *__restrict__ src = VS ? vrv : vtx;
     uint32_t t_cur = 0, t_nxt = 0, vi_nxt[3] = {0, 0, 0}, q_next = 0;
     float4 c_cur[3] = {make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0), make_float4(0, 0, 0, 0)};
@@ -1998,8 +1997,10 @@ __global__ void __launch_bounds__(256) k_tile_clip(const float4 *__restrict__ vt
         uint32_t t = 0;
         if (j < n) {
             t = clipq[b0 + j];
-            if (CL) t = cmap[t];
-            if (cperm) t = cperm[t];
+            if (CL) {
+                t = cmap[t];
+                if (cperm) t = cperm[t];
+            }
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 load_corner(vtx, vidx[3 * t + k], m, factor, half_w, half_h, d[k]);
@@ -3059,8 +3060,8 @@ template <bool VS, bool CL>
 void setup_launch(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, const TileClusters *cl, const Mat34 &m,
                   float factor, float sw, float sh, uint32_t band, uint32_t nparts, uint32_t part, uint32_t tx, uint32_t xoff,
                   void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, const float4 *vrv,
-                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap, const uint32_t *sperm = nullptr) {
-    const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : sperm, *tab = CL ? cl->shard : nullptr;
+                  hipStream_t st, uint32_t *tbin, uint32_t bin_cap) {
+    const uint32_t *cmap = CL ? cl->cmap : nullptr, *perm = CL ? cl->perm : nullptr, *tab = CL ? cl->shard : nullptr;
     { hipLaunchKernelGGL((k_tile_setup<VS, CL>), dim3(shard_grid(k_tile_setup<VS, CL>, ntri, CL ? 256 : 1024)), dim3(256),
                        0, st, vtx, vidx, ntri, cmap, perm, tab, m, factor, sw, sh, band, nparts, part, tx, xoff,
                        (RasterRec *)recs, live, clipq, ctr, counts, vrv, tbin, bin_cap); after_launch("k_tile_setup", st); }
@@ -3075,7 +3076,7 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        void *recs, uint4 *live, uint32_t *clipq, uint32_t *ctr, uint32_t *counts, uint32_t *offs,
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st, float4 *vrv,
                        uint32_t nv, const TileClusters *cl, uint32_t *sum_host, uint32_t tag, uint32_t *tbin,
-                       uint32_t bin_cap, uint32_t xoff, const uint32_t *sperm) {
+                       uint32_t bin_cap, uint32_t xoff) {
     const uint64_t ns = tile_slots(W, rows_local, xoff);  // (counts and ctr's shard counters: left zeroed)
     const bool clustered = cl && cl->ncl;
     if (vrv && nv && !clustered)
@@ -3092,7 +3093,7 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                                       ctr, counts, vrv, st, tbin, bin_cap);
         } else {
             setup_launch<false, false>(vtx, vidx, ntri, cl, m, factor, sw, sh, band, nparts, part, tx, xoff, recs, live,
-                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap, sperm);
+                                       clipq, ctr, counts, nullptr, st, tbin, bin_cap);
         }
     }
     if (bin_cap) {                                       // bins mode: binned already

@@ -43,8 +43,6 @@
 namespace s3r_host {   // clusters.cpp
 void build_clusters(const float *vtx, uint32_t nv, const uint32_t *vidx, uint32_t ntri, uint32_t kmin, uint32_t kmax,
                     std::vector<uint32_t> &first, std::vector<float> &sphere, std::vector<uint32_t> &perm);
-void spatial_order(const std::vector<uint32_t> &first, const std::vector<float> &sphere, const std::vector<uint32_t> &perm,
-                   uint32_t ntri, std::vector<uint32_t> &out);
 }
 namespace s3r_host {   // host_fill.cpp
 void fill_words(uint32_t *p, size_t n, uint32_t v);
@@ -243,9 +241,6 @@ constexpr uint64_t kNearCheckMaxTri = 1024;   // the host's near-plane check: sc
 constexpr uint32_t kDefaultBand = 16;       // rows per interleaved band when updateAndRender spans devices
 constexpr uint32_t kSumWords = 8;           // tile path: host-coherent summary words per buffer set
 constexpr int kMaxDevices = 64;
-#ifndef S3R_SPATIAL
-#define S3R_SPATIAL 1               // whole tile-path frames set triangles up in the clusters' Morton order
-#endif
 
 // S3R_HOSTPROF=1 (diagnostics): host time per s3r_render_bands section, printed at shutdown.
 struct HostProf {
@@ -301,7 +296,6 @@ struct Dev {
     // and the cull's per-frame position list (one: every tile-path setup runs on geo[0])
     float4 *cl_sphere = nullptr;
     uint32_t *cl_first = nullptr, *cl_perm = nullptr, *cl_shard = nullptr, *cl_map = nullptr;
-    uint32_t *sp_perm = nullptr;     // whole-frame setup order: the clusters in Morton order (clusters.cpp spatial_order)
     uint64_t tiles_cap = 0, tile_list_cap[kSets] = {};
     uint4 *deferred = nullptr;                 // fused raster + resolve: pixels whose winner needs a full setup
     size_t deferred_cap = 0;
@@ -369,7 +363,6 @@ struct HostScene {
     std::vector<uint8_t> disc;
     std::vector<uint32_t> vidx, aidx, tex;
     std::vector<uint32_t> cl_first, cl_perm;   // clusters (tile path): position ranges, position -> slot
-    std::vector<uint32_t> sp_perm;             // whole-frame setup order (spatial_order)
     std::vector<uint32_t> cl_shard;            // where each shard's positions start (cluster_shard_table)
     std::vector<float> cl_sphere;              // 4 per cluster: centre, radius
 };
@@ -709,7 +702,6 @@ HostScene read_scene() {
                                  (uint32_t)ntri, 8, 32, s.cl_first, s.cl_sphere, s.cl_perm);
     g.ncl = s.cl_first.empty() ? 0 : (uint32_t)s.cl_first.size() - 1;
     if (g.ncl) s.cl_shard = cluster_shard_table(s.cl_first);
-    if (g.ncl && S3R_SPATIAL) s3r_host::spatial_order(s.cl_first, s.cl_sphere, s.cl_perm, (uint32_t)ntri, s.sp_perm);
     return s;
 }
 
@@ -758,10 +750,6 @@ void dev_init(Dev &d, const HostScene &s) {
         HIPCHECK(hipMemcpy(d.cl_shard, s.cl_shard.data(), (kTileShards + 1) * 4, hipMemcpyHostToDevice));
         HIPCHECK(hipMemcpy(d.cl_sphere, s.cl_sphere.data(), (size_t)g.ncl * 16, hipMemcpyHostToDevice));
         HIPCHECK(hipMemcpy(d.cl_first, s.cl_first.data(), ((size_t)g.ncl + 1) * 4, hipMemcpyHostToDevice));
-        if (!s.sp_perm.empty()) {
-            d.sp_perm = dalloc<uint32_t>(ntri);
-            HIPCHECK(hipMemcpy(d.sp_perm, s.sp_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
-        }
         if (!s.cl_perm.empty()) {
             d.cl_perm = dalloc<uint32_t>(ntri);
             HIPCHECK(hipMemcpy(d.cl_perm, s.cl_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
@@ -845,7 +833,7 @@ void unregister_all() {
 void dev_release(Dev &d) {
     (void)hipSetDevice(d.device);
     void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
-                    d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq, d.sp_perm};
+                    d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int q = 0; q < kSets; q++) {      // tile_total aliases tile_ctr
@@ -1355,7 +1343,7 @@ void rebin(Dev &d, uint32_t p, uint32_t W, uint32_t H, uint32_t band, uint32_t n
                           d.recs[p], d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p],
                           d.tile_cursor[p], d.scan_temp, d.scan_temp_bytes, geo, d.vrv, g.nv, &cl,
                           d.tile_sum_dev + kSumWords * p, d.frame_no, bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u,
-                          d.tile_xoff, d.sp_perm);
+                          d.tile_xoff);
         wait_tile_summary(d, p, geo);
         if (!bins) {
             grow_tile_list(d, p, sum[2]);
@@ -1436,7 +1424,7 @@ void render_tiles(Dev &d, uint32_t W, uint32_t H, uint32_t band, uint32_t nparts
     launch_tile_setup(d.vtx, d.vidx, g.ntri, g.m, g.factor, sw, sh, W, band, nparts, part, rows_local, d.recs[p],
                       d.live[p], d.clipq, d.tile_ctr[p], d.tile_counts[p], d.tile_offs[p], d.tile_cursor[p], d.scan_temp,
                       d.scan_temp_bytes, geo, d.vrv, g.nv, &cl, d.tile_sum_dev + kSumWords * p, d.frame_no,
-                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff, d.sp_perm);
+                      bins ? d.tbin[p] : nullptr, bins ? d.bin_cap : 0u, d.tile_xoff);
     // The list size is data-dependent.  Asynchronous frames (s3r_render_bands), and the first frame
     // of each buffer set, read it back before the fill (one host sync); synchronous frames
     // (updateAndRender) fill the set's list as sized by earlier frames, with no sync, and are

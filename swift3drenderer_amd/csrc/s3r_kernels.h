@@ -167,11 +167,9 @@ void launch_tile_setup(const float4 *vtx, const uint32_t *vidx, uint32_t ntri, c
                        uint32_t *cursor, void *scan_temp, size_t scan_temp_bytes, hipStream_t st,
                        float4 *vrv = nullptr, uint32_t nv = 0, const TileClusters *cl = nullptr,
                        uint32_t *sum_host = nullptr, uint32_t tag = 0, uint32_t *tbin = nullptr, uint32_t bin_cap = 0,
-                       uint32_t xoff = 0, const uint32_t *sperm = nullptr);
+                       uint32_t xoff = 0);
 // No raster record is written for the slots the raster can set up again from the scene (kernels.hip
-// kNoRecBit); the clip's slots keep theirs.  sperm (may be null; used without clusters and without the
-// vertex stage): the setup's processing order, position -> slot (render_api.cpp sp_perm) -- any
-// permutation gives the same pixels.
+// kNoRecBit); the clip's slots keep theirs.
 // tbin / bin_cap (bins mode): every (tile, bucket) slot s gets bin_cap entries at tbin + s x bin_cap
 // and counts[s] of them filled by the setup itself -- no scan, no fill pass; the summary's word 4 is
 // then the count the fullest slot needed when it exceeded bin_cap (0: none; the frame is rendered

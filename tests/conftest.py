@@ -39,3 +39,19 @@ def gpu_renderer():
         pytest.skip('no GPU')
     from swift3drenderer_amd.renderer import Renderer
     return Renderer()
+
+
+@pytest.fixture(autouse=True)
+def _gpu_output_uncaptured(request):
+    """GPU tests run with pytest's fd capture off: a library that ends the process (a device fault's
+    HIPCHECK abort, a bounded wait's stall exit) prints its reason to stderr first, and a captured
+    stderr dies with the process -- the round-4 aborts lost their messages that way."""
+    if request.node.get_closest_marker('gpu') is None:
+        yield
+        return
+    capman = request.config.pluginmanager.getplugin('capturemanager')
+    if capman is None:
+        yield
+        return
+    with capman.global_and_fixture_disabled():
+        yield

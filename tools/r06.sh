@@ -3,7 +3,7 @@
 # Every step writes its stdout AND stderr to its own file under gpurun_out/r06/ (nothing discarded,
 # nothing held back in a pipe, so a stalled step leaves what it printed), runs under its own time limit,
 # and a failing step ends the call (no retries).  Variant libraries come from tools/variants.py build.
-OUT=gpurun_out/r06
+OUT=${OUT_R06:-gpurun_out/r06}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 STRESS=/tmp/s3r_stress.bin
@@ -127,15 +127,30 @@ for k, c in json.load(open('$OUT/spab_pmc_$v/pmc_summary.json')).items():
     if 'k_tile' in k: print('  $v %-44s FETCH %.1f MB  WRITE %.1f MB' % (k[-44:], c.get('FETCH_SIZE', 0) / 1024, c.get('WRITE_SIZE', 0) / 1024))"
       done
       ;;
+    eighth)   # per-stage breakdown of part 0 of 8 at 4K and 8K (pipelined frames, kernel trace + host enqueue)
+      for sz in "3840 2160" "7680 4320"; do
+        set -- $sz
+        tag=eighth_$1
+        step ${tag}_probe 120 python3 -u tools/overhead_probe.py --width $1 --height $2 --nparts 8 --steps 2000 || exit 1
+        H=$(python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/${tag}_probe.log') if l.startswith('{')][-1]
+print(round(d['host_enqueue_us'], 2))")
+        step ${tag}_trace 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/${tag}_trace" -o run -- \
+            python3 tools/overhead_probe.py --width $1 --height $2 --nparts 8 --steps 2000 || exit 1
+        f=$(find "$OUT/${tag}_trace" -name '*kernel_trace.csv' | sort | tail -1)
+        python3 tools/eighth_breakdown.py "$f" --frames 1000 --host-us $H --label "part 0 of 8, $1x$2" | tee "$OUT/${tag}_breakdown.json"
+      done
+      ;;
     rowparity)   # the row path's parity suite
-      step rowparity 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+      step rowparity 600 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu \
           tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
       ;;
     stall)   # the bounded-wait tests (each a child process that must end with status 86)
-      step stall 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_stall.py || exit 1
+      step stall 300 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu tests/test_stall.py || exit 1
       ;;
     tiles)   # the tile path's parity suite
-      step tiles 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_tiles.py || exit 1
+      step tiles 900 python3 -u -m pytest -s -x -v --timeout 300 --timeout-method thread -m gpu tests/test_tiles.py || exit 1
       ;;
     stress)  # config 5 (1 M icosahedra, 4K, tile path): the bench line, part 0 of 8 at the library's band
       [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
@@ -156,7 +171,7 @@ for l in open('$OUT/parts_all.jsonl'):
     d=json.loads(l); print('  config', d['config'], 'N', d['N'], 'band', d['band'], 'slowest', d['slowest_us'], 'max/mean', d['max_over_mean'], 'eff', d['efficiency_per_gpu'])"
       ;;
     suite)   # the whole GPU suite, once
-      step suite 1100 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests || exit 1
+      step suite 1100 python3 -u -m pytest -s -x -v --timeout 200 --timeout-method thread -m gpu tests || exit 1
       ;;
     *) echo "unknown recipe $recipe"; exit 2 ;;
   esac
