@@ -142,6 +142,19 @@ print(round(d['host_enqueue_us'], 2))")
         python3 tools/eighth_breakdown.py "$f" --frames 1000 --host-us $H --label "part 0 of 8, $1x$2" | tee "$OUT/${tag}_breakdown.json"
       done
       ;;
+    seg8k)   # part 0 of 8 of the 8K and 4K frames under fragment segment widths (S3R_MIN_BLOCKS / S3R_SEG3)
+      for cfg in "7680 4320 S3R_NOTHING=0" "7680 4320 S3R_SEG3=1 S3R_MIN_BLOCKS=3000" "7680 4320 S3R_MIN_BLOCKS=6000" \
+                 "7680 4320 S3R_MIN_BLOCKS=10000" "3840 2160 S3R_NOTHING=0" "3840 2160 S3R_SEG3=1 S3R_MIN_BLOCKS=1300"; do
+        set -- $cfg
+        w=$1; h=$2; shift 2
+        tag=seg_${w}_$(echo "$*" | tr ' =' '__')
+        step $tag 120 env "$@" python3 -u tools/overhead_probe.py --width $w --height $h --nparts 8 --steps 2000 || exit 1
+        python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/$tag.log') if l.startswith('{')][-1]
+print('  $w $*: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 2), 'host_us', round(d['host_enqueue_us'], 2))"
+      done
+      ;;
     rowparity)   # the row path's parity suite
       step rowparity 600 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu \
           tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
