@@ -735,6 +735,18 @@ void dev_init(Dev &d, const HostScene &s) {
     HIPCHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
     // (the default priority instead measured the same for pipelined HBM frames, profiles/r05_order_ab.txt)
     for (hipStream_t &gs : d.geo) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
+    // (a fault pending from before -- the previous scene's release, its allocations -- is reported here
+    // as such, not by the uploads below; round 4 and round 6 each saw one illegal-address error at the
+    // third upload of a scene load in the tile suite)
+    {
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            fprintf(stderr, "s3r: HIP error %s on device %d before the scene upload (a fault pending from the "
+                    "previous scene's release or this scene's allocations)\n", hipGetErrorName(e), d.device);
+            fflush(stderr);
+            abort();
+        }
+    }
     HIPCHECK(hipMemcpy(d.vtx, s.vtx.data(), (size_t)g.nv * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d.nrm, s.nrm.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d.pay, s.pay.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
@@ -830,33 +842,53 @@ void unregister_all() {
     g.reg_epoch++;
 }
 
+// Every call's status is checked (round 6: a device fault that surfaced at the third upload of the
+// next scene could have been raised -- and discarded -- here); the first failure is reported with
+// the call and the device, then the process aborts.
 void dev_release(Dev &d) {
-    (void)hipSetDevice(d.device);
+    hipError_t first = hipSuccess;
+    const char *what = "";
+    auto chk = [&](hipError_t e, const char *w) {
+        if (e != hipSuccess && first == hipSuccess) { first = e; what = w; }
+    };
+    chk(hipSetDevice(d.device), "hipSetDevice");
     void *ptrs[] = {d.vtx, d.nrm, d.pay, d.disc, d.vidx, d.aidx, d.tex, d.frame, d.deferred, d.scan_temp, d.vrv, d.geo_cnt,
                     d.cl_sphere, d.cl_first, d.cl_perm, d.cl_map, d.cl_shard, d.clipq};
     for (void *p : ptrs)
-        if (p) (void)hipFree(p);
+        if (p) chk(hipFree(p), "hipFree (scene / frame buffers)");
     for (int q = 0; q < kSets; q++) {      // tile_total aliases tile_ctr
         void *set[] = {d.tris[q], d.rowtab[q], d.bincnt[q], d.pairs[q], d.order[q], d.tile_counts[q], d.tile_offs[q],
                        d.tile_cursor[q], d.tile_list[q], d.recs[q], d.live[q], d.tile_ctr[q], d.tbin[q]};
         for (void *p : set)
-            if (p) (void)hipFree(p);
+            if (p) chk(hipFree(p), "hipFree (buffer sets)");
     }
-    if (d.done_host) (void)hipHostFree((void *)d.done_host);
-    if (d.handoff) (void)hipEventDestroy(d.handoff);
-    if (d.tile_sum_host) (void)hipHostFree(d.tile_sum_host);
-    if (d.fill_flags) (void)hipHostFree(d.fill_flags);
-    if (d.fill_chunks) (void)hipHostFree(d.fill_chunks);
+    if (d.done_host) chk(hipHostFree((void *)d.done_host), "hipHostFree (completion and error words)");
+    if (d.handoff) chk(hipEventDestroy(d.handoff), "hipEventDestroy");
+    if (d.tile_sum_host) chk(hipHostFree(d.tile_sum_host), "hipHostFree (tile summary)");
+    if (d.fill_flags) chk(hipHostFree(d.fill_flags), "hipHostFree (fill flags)");
+    if (d.fill_chunks) chk(hipHostFree(d.fill_chunks), "hipHostFree (fill chunk masks)");
     for (int p = 0; p < kSets; p++) {
-        if (d.geo_done[p]) (void)hipEventDestroy(d.geo_done[p]);
-        if (d.frag_done[p]) (void)hipEventDestroy(d.frag_done[p]);
+        if (d.geo_done[p]) chk(hipEventDestroy(d.geo_done[p]), "hipEventDestroy");
+        if (d.frag_done[p]) chk(hipEventDestroy(d.frag_done[p]), "hipEventDestroy");
     }
     for (hipStream_t gs : d.geo)
-        if (gs) (void)hipStreamDestroy(gs);
+        if (gs) chk(hipStreamDestroy(gs), "hipStreamDestroy (geometry)");
     for (auto &t : d.tslots) {
-        (void)hipEventDestroy(t.frame0); (void)hipEventDestroy(t.frag0); (void)hipEventDestroy(t.frag1);
+        chk(hipEventDestroy(t.frame0), "hipEventDestroy"); chk(hipEventDestroy(t.geo1), "hipEventDestroy");
+        chk(hipEventDestroy(t.frag0), "hipEventDestroy"); chk(hipEventDestroy(t.frag1), "hipEventDestroy");
     }
-    if (d.stream) (void)hipStreamDestroy(d.stream);
+    if (d.stream) chk(hipStreamDestroy(d.stream), "hipStreamDestroy");
+    // the frees and destructions above complete before anything else runs on the device
+    if (first == hipSuccess) {
+        Watchdog::Guard guard(WaitSite{"release: after freeing the device's memory", "the device", d.device, d.frame_no});
+        chk(hipDeviceSynchronize(), "hipDeviceSynchronize after the frees");
+    }
+    if (first != hipSuccess) {
+        fprintf(stderr, "s3r: HIP error %s from %s on device %d while releasing the library's memory\n",
+                hipGetErrorName(first), what, d.device);
+        fflush(stderr);
+        abort();
+    }
 }
 
 void release_all() {

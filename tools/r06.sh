@@ -155,6 +155,24 @@ d=[json.loads(l) for l in open('$OUT/$tag.log') if l.startswith('{')][-1]
 print('  $w $*: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 2), 'host_us', round(d['host_enqueue_us'], 2))"
       done
       ;;
+    timeline)   # per-workgroup k_fragment timelines (timing build build/librender_wgt.so): 8K and 4K eighths, 4K whole
+      step tl_8k_n8 240 python3 -u tools/wg_timeline.py --width 7680 --height 4320 --nparts 8 || exit 1
+      step tl_4k_n8 240 python3 -u tools/wg_timeline.py --nparts 8 || exit 1
+      step tl_8k_n1 240 python3 -u tools/wg_timeline.py --width 7680 --height 4320 || exit 1
+      grep -h "launch span\|total\|in flight" "$OUT"/tl_*.log
+      ;;
+    nobin)   # config 5 whole frame, serialised kernel times: product vs the no-binning ablation (wrong pixels)
+      [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
+      for v in prod nobin; do
+        L=""; [ $v = nobin ] && L=build/librender_nobin.so
+        step nobin_k_$v 300 env ${L:+S3R_LIB=$L} S3R_SERIAL=1 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nobin_k_$v" -o run -- \
+            python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $STRESS --steps 20 || exit 1
+        f=$(find "$OUT/nobin_k_$v" -name '*kernel_stats.csv' | sort | tail -1)
+        python3 -c "
+import csv
+for r in list(csv.DictReader(open('$f')))[:4]: print('  $v %-50s %6s calls avg %9.1f us' % (r['Name'][:50], r['Calls'], float(r['AverageNs'])/1e3))"
+      done
+      ;;
     rowparity)   # the row path's parity suite
       step rowparity 600 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu \
           tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
