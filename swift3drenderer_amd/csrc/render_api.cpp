@@ -705,6 +705,27 @@ HostScene read_scene() {
     return s;
 }
 
+// The scene's upload: every array copied through one page-locked staging buffer of the library's own
+// (hipHostMalloc) in 16-MiB pieces on the device's stream.  Not the runtime's pageable hipMemcpy:
+// that path may take a source address for user memory a registration once covered (the tests free
+// caller buffers the library had page-locked, and the heap reuses their addresses) -- round 4 and
+// round 6 each saw an illegal-address error at a scene load's third upload.
+struct Uploader {
+    static constexpr size_t kPiece = 16u << 20;
+    Dev &d;
+    void *stage = nullptr;
+    explicit Uploader(Dev &dev) : d(dev) { HIPCHECK(hipHostMalloc(&stage, kPiece, hipHostMallocDefault)); }
+    ~Uploader() { if (stage) (void)hipHostFree(stage); }
+    void put(void *dst, const void *src, size_t bytes) {
+        for (size_t o = 0; o < bytes; o += kPiece) {
+            const size_t n = std::min(kPiece, bytes - o);
+            memcpy(stage, static_cast<const uint8_t *>(src) + o, n);
+            HIPCHECK(hipMemcpyAsync(static_cast<uint8_t *>(dst) + o, stage, n, hipMemcpyHostToDevice, d.stream));
+            sync_stream(d.stream, WaitSite{"scene upload", "a host-to-device copy", d.device, 0u});
+        }
+    }
+};
+
 void dev_init(Dev &d, const HostScene &s) {
     HIPCHECK(hipSetDevice(d.device));
     HIPCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -734,6 +755,7 @@ void dev_init(Dev &d, const HostScene &s) {
     int prio_least = 0, prio_greatest = 0;
     HIPCHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
     // (the default priority instead measured the same for pipelined HBM frames, profiles/r05_order_ab.txt)
+    // (round 6, frame parts: the default priority measured the same, profiles/r06_part_negatives.txt)
     for (hipStream_t &gs : d.geo) HIPCHECK(hipStreamCreateWithPriority(&gs, hipStreamNonBlocking, prio_greatest));
     // (a fault pending from before -- the previous scene's release, its allocations -- is reported here
     // as such, not by the uploads below; round 4 and round 6 each saw one illegal-address error at the
@@ -747,24 +769,25 @@ void dev_init(Dev &d, const HostScene &s) {
             abort();
         }
     }
-    HIPCHECK(hipMemcpy(d.vtx, s.vtx.data(), (size_t)g.nv * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.nrm, s.nrm.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.pay, s.pay.data(), (size_t)g.na * 16, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.disc, s.disc.data(), g.na, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.vidx, s.vidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.aidx, s.aidx.data(), 12 * (size_t)ntri, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(d.tex, s.tex.data(), (size_t)g.ntex * 4, hipMemcpyHostToDevice));
+    Uploader up(d);
+    up.put(d.vtx, s.vtx.data(), (size_t)g.nv * 16);
+    up.put(d.nrm, s.nrm.data(), (size_t)g.na * 16);
+    up.put(d.pay, s.pay.data(), (size_t)g.na * 16);
+    up.put(d.disc, s.disc.data(), g.na);
+    up.put(d.vidx, s.vidx.data(), 12 * (size_t)ntri);
+    up.put(d.aidx, s.aidx.data(), 12 * (size_t)ntri);
+    up.put(d.tex, s.tex.data(), (size_t)g.ntex * 4);
     if (g.ncl) {
         d.cl_sphere = dalloc<float4>(g.ncl);
         d.cl_first = dalloc<uint32_t>((size_t)g.ncl + 1);
         d.cl_map = dalloc<uint32_t>(ntri);
         d.cl_shard = dalloc<uint32_t>(kTileShards + 1);
-        HIPCHECK(hipMemcpy(d.cl_shard, s.cl_shard.data(), (kTileShards + 1) * 4, hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(d.cl_sphere, s.cl_sphere.data(), (size_t)g.ncl * 16, hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(d.cl_first, s.cl_first.data(), ((size_t)g.ncl + 1) * 4, hipMemcpyHostToDevice));
+        up.put(d.cl_shard, s.cl_shard.data(), (kTileShards + 1) * 4);
+        up.put(d.cl_sphere, s.cl_sphere.data(), (size_t)g.ncl * 16);
+        up.put(d.cl_first, s.cl_first.data(), ((size_t)g.ncl + 1) * 4);
         if (!s.cl_perm.empty()) {
             d.cl_perm = dalloc<uint32_t>(ntri);
-            HIPCHECK(hipMemcpy(d.cl_perm, s.cl_perm.data(), (size_t)ntri * 4, hipMemcpyHostToDevice));
+            up.put(d.cl_perm, s.cl_perm.data(), (size_t)ntri * 4);
         }
     }
 }

@@ -173,6 +173,49 @@ import csv
 for r in list(csv.DictReader(open('$f')))[:4]: print('  $v %-50s %6s calls avg %9.1f us' % (r['Name'][:50], r['Calls'], float(r['AverageNs'])/1e3))"
       done
       ;;
+    bands)   # every part of the 8-way split of configs 4 and 3 at several band heights
+      for b in 8 16 32 64; do
+        step bands_$b 300 python3 -u tools/parts_all.py --configs 4,3 --nparts 1,8 --band $b --out "$OUT/bands_$b.jsonl" || exit 1
+        python3 -c "
+import json
+for l in open('$OUT/bands_$b.jsonl'):
+    d=json.loads(l); print('  band $b config', d['config'], 'N', d['N'], 'slowest', d['slowest_us'], 'max/mean', d['max_over_mean'], 'eff', d['efficiency_per_gpu'])"
+      done
+      ;;
+    geovar)   # configs 4 and 3, whole frame and every eighth, for geometry variants (VARIANTS="tag tag ...")
+      for rep in 1 2; do
+        for v in prod ${VARIANTS:-geoprio0 georows256 georows64}; do
+          L=""; [ $v != prod ] && L=build/librender_$v.so
+          step geovar_${v}_$rep 300 env ${L:+S3R_LIB=$L} python3 -u tools/parts_all.py --configs 4,3 --nparts 1,8 --out "$OUT/geovar_${v}_$rep.jsonl" || exit 1
+          python3 -c "
+import json
+for l in open('$OUT/geovar_${v}_$rep.jsonl'):
+    d=json.loads(l); print('  $v rep $rep config', d['config'], 'N', d['N'], 'slowest', d['slowest_us'], 'eff', d['efficiency_per_gpu'])"
+        done
+      done
+      ;;
+    split)   # the split k_fragment instance (S3R_SPLIT_BINS): parity forced on every HBM launch, then part 0 of 8
+      step split_parity 600 env S3R_SPLIT_BINS=100000000 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu \
+          tests/test_gpu_parity.py tests/test_multi_device.py tests/test_multi.py tests/test_stream_order.py || exit 1
+      for sz in "7680 4320" "3840 2160"; do
+        set -- $sz
+        for sb in 0 3000; do
+          tag=split_${1}_$sb
+          step $tag 120 env S3R_SPLIT_BINS=$sb python3 -u tools/overhead_probe.py --width $1 --height $2 --nparts 8 --steps 2000 || exit 1
+          python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/$tag.log') if l.startswith('{')][-1]
+print('  $1 split_bins $sb: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 2), 'host_us', round(d['host_enqueue_us'], 2))"
+        done
+      done
+      for sb in 0 3000 0 3000; do
+        step split_parts_$sb 300 env S3R_SPLIT_BINS=$sb python3 -u tools/parts_all.py --configs 4,3 --nparts 1,8 --out "$OUT/split_parts_$sb.jsonl" || exit 1
+        python3 -c "
+import json
+for l in open('$OUT/split_parts_$sb.jsonl'):
+    d=json.loads(l); print('  split_bins $sb config', d['config'], 'N', d['N'], 'slowest', d['slowest_us'], 'eff', d['efficiency_per_gpu'])"
+      done
+      ;;
     rowparity)   # the row path's parity suite
       step rowparity 600 python3 -u -m pytest -s -x -v --timeout 120 --timeout-method thread -m gpu \
           tests/test_gpu_parity.py tests/test_multi_device.py || exit 1
