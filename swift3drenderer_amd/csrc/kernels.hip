@@ -1880,6 +1880,104 @@ __device__ __forceinline__ void emit_slot(bool live, const TriSetup &ts, const V
 }
 
 
+// Bins mode, workgroup-aggregated (k_tile_setup): one iteration's entries of the workgroup's 256
+// triangles grouped by their (tile, bucket) key in an LDS hash table -- LDS atomics count them, then
+// ONE returning global atomic per distinct key reserves the key's run in its bin, and the entries are
+// written as one contiguous run per key.  The per-wave form before (tile_visit: runs of equal keys among
+// adjacent lanes, a returning global atomic per run) paid a global atomic -- a memory-side round trip
+// (MI355X_MICROARCH.md) -- per few entries: stress scene, the binning took ~240 of the setup's 424 us
+// (no-binning ablation, profiles/r06_bin_agg_ab.txt).  A key that finds the table full takes the
+// per-entry path (a returning atomic of its own).
+#ifndef S3R_BIN_AGG
+#define S3R_BIN_AGG 1
+#endif
+constexpr uint32_t kAggSlots = 1024, kAggEmpty = 0xFFFFFFFFu, kAggFull = 0xFFFFFFFFu, kAggProbes = 16;
+struct BinAgg {
+    uint32_t key[kAggSlots];         // kAggEmpty: free
+    uint32_t cnt[kAggSlots];         // entries counted, then (after the reservation) the run's cursor
+    uint32_t base[kAggSlots];        // the run's first position in its bin
+    uint32_t used[kAggSlots];        // the occupied slots, in insertion order
+    uint32_t nused;
+};
+__device__ __forceinline__ uint32_t agg_hash(uint32_t k) { return (k * 0x9E3779B1u) >> 22; }   // 10 bits
+__device__ __forceinline__ uint32_t agg_insert(BinAgg &a, uint32_t key) {
+    uint32_t h = agg_hash(key);
+    for (uint32_t i = 0; i < kAggProbes; i++, h = (h + 1u) & (kAggSlots - 1u)) {
+        const uint32_t prev = atomicCAS(&a.key[h], kAggEmpty, key);
+        if (prev == kAggEmpty) { a.used[atomicAdd(&a.nused, 1u)] = h; return h; }
+        if (prev == key) return h;
+    }
+    return kAggFull;
+}
+__device__ __forceinline__ uint32_t agg_find(const BinAgg &a, uint32_t key) {
+    uint32_t h = agg_hash(key);
+    for (uint32_t i = 0; i < kAggProbes; i++, h = (h + 1u) & (kAggSlots - 1u)) {
+        const uint32_t k = a.key[h];
+        if (k == key) return h;
+        if (k == kAggEmpty) break;
+    }
+    return kAggFull;
+}
+// the (tile, bucket) key of entry k of span sp
+__device__ __forceinline__ uint32_t span_key(const TileSpan &sp, uint32_t k, uint32_t tiles_x) {
+    uint32_t ky = udiv_small(k, udiv_inv(sp.ntx));
+    if (sp.n >= (1u << 18)) ky = k / sp.ntx;            // (beyond udiv_small's range: huge boxes)
+    return ((sp.ty0 + ky) * tiles_x + sp.tx0 + k - ky * sp.ntx) * kDepthBuckets + sp.bucket;
+}
+// The slot's span (its tiles in this part's rows, and its depth bucket), as emit_slot computes it.
+__device__ __forceinline__ TileSpan slot_span(bool live, const TriSetup &ts, uint32_t band, uint32_t nparts,
+                                              uint32_t part, uint32_t xoff) {
+    TileSpan sp{0, 1, 0, 0, 0};
+    if (!live) return sp;
+    sp = box_tiles(tile_box(ts.xmin | (ts.xmax << 16), 0u, xoff), ts.ymin | (ts.ymax << 16), band, nparts, part);
+    if (sp.n) sp.bucket = tile_box(ts.xmin | (ts.xmax << 16), f2u(ooz_bound(ts)), xoff) >> 24;
+    return sp;
+}
+// One iteration's entries of the whole workgroup (every thread calls it, with n = 0 for none):
+// entry k of lane's span holds `slot`.  Three barriers; the table is left empty.
+__device__ void bin_agg(BinAgg &a, const TileSpan &sp, uint32_t slot, uint32_t tiles_x, uint32_t *__restrict__ counts,
+                        uint32_t *__restrict__ tbin, uint32_t bin_cap, uint32_t *__restrict__ ovf) {
+    // count
+    for (uint32_t k = 0; k < sp.n; k++) {
+        const uint32_t key = span_key(sp, k, tiles_x);
+        const uint32_t h = agg_insert(a, key);
+        if (h != kAggFull) {
+            atomicAdd(&a.cnt[h], 1u);
+        } else {                                         // table full: this entry on its own
+            const uint32_t b = atomicAdd(&counts[key], 1u);
+            if (b < bin_cap) tbin[(size_t)key * bin_cap + b] = slot;
+            else atomicMax(ovf, b + 1u);
+        }
+    }
+    __syncthreads();
+    // reserve each key's run (one returning global atomic per key)
+    const uint32_t nu = a.nused;
+    for (uint32_t i = threadIdx.x; i < nu; i += blockDim.x) {
+        const uint32_t h = a.used[i], c = a.cnt[h];
+        const uint32_t b = atomicAdd(&counts[a.key[h]], c);
+        if (b + c > bin_cap) atomicMax(ovf, b + c);
+        a.base[h] = b;
+        a.cnt[h] = 0u;
+    }
+    __syncthreads();
+    // write the runs
+    for (uint32_t k = 0; k < sp.n; k++) {
+        const uint32_t key = span_key(sp, k, tiles_x);
+        const uint32_t h = agg_find(a, key);
+        if (h == kAggFull) continue;                     // (written above)
+        const uint32_t pos = a.base[h] + atomicAdd(&a.cnt[h], 1u);
+        if (pos < bin_cap) tbin[(size_t)key * bin_cap + pos] = slot;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nu; i += blockDim.x) {
+        const uint32_t h = a.used[i];
+        a.key[h] = kAggEmpty;
+        a.cnt[h] = 0u;
+    }
+    if (threadIdx.x == 0) a.nused = 0u;
+    __syncthreads();
+}
+
 // Setup, one lane per triangle; workgroup b serves shard s = b % kTileShards, grid-stride over the
 // shard's positions p = base(s) + j (with clusters: the cull's kept positions cmap[p], each one's slot
 // cperm[cmap[p]] -- the identity when cperm is null -- loaded one iteration ahead; without: slot p).
@@ -1917,6 +2015,15 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
     // cull's position for the iteration after that -- an iteration's loads are in flight while the
     // iteration before sets up and bins its triangles, so a wave waits on no load chain
     const uint32_t step = per * 256u, jl = rank * 256u + threadIdx.x;
+    __shared__ BinAgg agg;
+    // (whole frames only: frame parts, their clusters culled, set few triangles up per iteration, and
+    // the table's barriers cost more there than the atomics they save -- stress part 0 of 8 -5 %)
+    const bool aggregate = S3R_BIN_AGG && !CL && tbin != nullptr;
+    if (aggregate) {
+        for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) { agg.key[i] = kAggEmpty; agg.cnt[i] = 0u; }
+        if (threadIdx.x == 0) agg.nused = 0u;
+        __syncthreads();
+    }
     auto slot_at = [&](uint32_t jj, uint32_t q) { return CL ? (cperm ? cperm[q] : q) : b0 + jj; };
     const float4 *__restrict__ src = VS ? vrv : vtx;
     uint32_t t_cur = 0, t_nxt = 0, vi_nxt[3] = {0, 0, 0}, q_next = 0;
@@ -1932,8 +2039,11 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
         for (int k = 0; k < 3; k++) vi_nxt[k] = vidx[3 * t_nxt + k];
     }
     if (CL && jl + 2u * step < n) q_next = cmap[b0 + jl + 2u * step];
-    for (uint32_t j0 = rank * 256u + (threadIdx.x & ~63u); j0 < n; j0 += step) {   // wave-uniform
-        const uint32_t j = j0 + lane;
+    // aggregated binning: a workgroup-uniform trip count (its barriers) -- every wave runs while the
+    // workgroup's first position is below n; otherwise each wave stops at its own end
+    const uint32_t wofs = aggregate ? 0u : (threadIdx.x & ~63u);
+    for (uint32_t wb = rank * 256u; wb + wofs < n; wb += step) {
+        const uint32_t j = wb + threadIdx.x;
         Vert d[3];
         TriSetup ts;
         bool live_t = false, clip = false;
@@ -1963,8 +2073,12 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
-        emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4,
-                  false);
+        if (aggregate)
+            bin_agg(agg, slot_span(live_t, ts, band, nparts, part, xoff), t | kNoRecBit, tiles_x, counts, tbin, bin_cap,
+                    ctr + 4);
+        else
+            emit_slot(live_t, ts, d, t, band, nparts, part, tiles_x, xoff, recs, lv, nlive, counts, tbin, bin_cap, ctr + 4,
+                      false);
     }
 }
 

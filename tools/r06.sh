@@ -103,10 +103,11 @@ print('  $1 $envs: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['
         done
       done
       ;;
-    spab)  # config 5 whole frame: the setup in the clusters' Morton order (product) vs file order (build S3R_SPATIAL=0)
+    spab|stressab)  # config 5 whole frame: product vs the variant build/librender_$AB.so (spab: AB=sp0)
+      [ $recipe = spab ] && AB=sp0
       [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
-      for v in prod sp0; do
-        L=""; [ $v = sp0 ] && L=build/librender_sp0.so
+      for v in prod $AB; do
+        L=""; [ $v = $AB ] && L=build/librender_$AB.so
         step spab_bench_$v 300 env ${L:+S3R_LIB=$L} python3 -u bench.py --scene icosa-stress --pose P_id --data $STRESS --no-cpu-baseline || exit 1
         grep '^{' "$OUT/spab_bench_$v.log" | tail -1 > "$OUT/spab_bench_$v.json"
         python3 -c "import json; d=json.load(open('$OUT/spab_bench_$v.json')); print('  $v stress', round(d['value']), 'fps  device', round(d['device_fps']), 'setup_ms', d['setup_ms'], 'frag_ms', d['fragment_kernel_ms'])"
@@ -214,6 +215,17 @@ print('  $1 split_bins $sb: part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', 
 import json
 for l in open('$OUT/split_parts_$sb.jsonl'):
     d=json.loads(l); print('  split_bins $sb config', d['config'], 'N', d['N'], 'slowest', d['slowest_us'], 'eff', d['efficiency_per_gpu'])"
+      done
+      ;;
+    stresspart)   # config 5: part 0 of 8 at the library's band, product vs build/librender_$AB.so
+      [ -f $STRESS ] || step stress_data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$STRESS')" || exit 1
+      for v in prod $AB prod $AB; do
+        L=""; [ $v = $AB ] && L=build/librender_$AB.so
+        step stresspart_$v 300 env ${L:+S3R_LIB=$L} python3 -u tools/overhead_probe.py --scene icosa-stress --pose P_id --data $STRESS --nparts 8 --band 135 --steps 100 || exit 1
+        python3 -c "
+import json
+d=[json.loads(l) for l in open('$OUT/stresspart_$v.log') if l.startswith('{')][-1]
+print('  $v stress part 0/8', round(1e6/d['wall_us']), 'fps  frag_us', round(d['frag_us'], 1))"
       done
       ;;
     rowparity)   # the row path's parity suite
