@@ -2664,6 +2664,32 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
     }
 #endif
     __syncthreads();
+#ifdef S3R_STATS
+    {
+        // the resolve's winners: foreground pixels, runs of one winner along a row (lane = column),
+        // and per wave (its 4 rows) ceil(runs / 64) -- the setup rounds a run-shared resolve would take
+        uint32_t fg = 0, runs = 0;
+        for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {
+            const uint32_t rr = i / kTileW, cc = i % kTileW;
+            const bool in = tr0 + rr <= tr1 && lx0 + cc <= lx1;
+            const unsigned long long k = in ? ls.key[rr * kKeyStride + cc] : 0ull;
+            const uint32_t sl = k ? (uint32_t)k : 0u;
+            const uint32_t left = (uint32_t)__shfl_up((int)sl, 1);
+            fg += sl ? 1u : 0u;
+            runs += (sl && (lane == 0u || left != sl)) ? 1u : 0u;
+        }
+        uint32_t v[2] = {fg, runs};
+        for (int k = 0; k < 2; k++)
+            for (int o = 32; o > 0; o >>= 1) v[k] += (uint32_t)__shfl_xor((int)v[k], o);
+        if (lane == 0) {
+            atomicAdd(&g_stats[2], (unsigned long long)v[0]);
+            atomicAdd(&g_stats[3], (unsigned long long)v[1]);
+            atomicAdd(&g_stats[4], (unsigned long long)((v[1] + 63u) / 64u));
+            atomicAdd(&g_stats[5], 1ull);
+            atomicMax(&g_stats[6], (unsigned long long)v[1]);
+        }
+    }
+#endif
     {
         for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {   // (wave-uniform trip count)
             const uint32_t rr = i / kTileW, cc = i % kTileW;
@@ -2672,7 +2698,11 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
             const unsigned long long k = in ? ls.key[rr * kKeyStride + cc] : 0ull;
             const uint32_t y = row_of(lr);
             uint32_t v = kBackground;
+#if defined(S3R_TABLATE) && (S3R_TABLATE & 8)
+            if (in) v = (uint32_t)k & 0xFFFFFFu;                // ablation: no resolve (timing only)
+#else
             if (in) v = resolve_pixel<true, true>(sc, k, x, y);
+#endif
             const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
 #ifdef S3R_BOUNDS
             if (in && idx >= (size_t)W * (frame_rows ? (uint32_t)sc.sh : rows_local)) {

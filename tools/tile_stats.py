@@ -31,6 +31,9 @@ def main():
     pairs = r.scene_counts()[5]
     print(f'{a.scene}/{a.pose} {a.width}x{a.height}: (slot, tile) pairs {pairs}, staged with rows {out[0]}, '
           f'culled by depth {out[1]} ({100.0 * out[1] / max(out[0], 1):.1f}%)')
+    print(f'resolve: foreground pixels {out[2]}, runs of one winner along a row {out[3]} '
+          f'({out[2] / max(out[3], 1):.2f} px per run), wave setup rounds run-shared {out[4]} of {4 * out[5]} '
+          f'per-pixel (waves {out[5]}, most runs in one wave {out[6]})')
     r.shutdown()
 
 
