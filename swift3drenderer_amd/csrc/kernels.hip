@@ -1471,23 +1471,30 @@ static_assert(kTileStage <= kTileThreads, "one staged triangle per thread at mos
 constexpr uint32_t kKeyStride = kTileW + 1;        // padded LDS row: rows of one column hit different banks
 constexpr uint32_t kDeadBox = 0xFFFFFFFFu;
 
-// Depth buckets of a tile's list (nearest first).  A listed triangle's bucket is the half-octave of
+// Depth buckets of a tile's list (nearest first).  A listed triangle's bucket is the eighth-octave of
 // its 1/z bound (ooz_bound) below 1/near = 10, the largest 1/z any pixel can have: bucket
-// b = (bits(10) >> 22) - (bits(bound) >> 22), clamped to [0, kDepthBuckets): 16 octaves, z up to
+// b = (bits(10) >> 20) - (bits(bound) >> 20), clamped to [0, kDepthBuckets): 16 octaves, z up to
 // ~6 500.  Every bound in bucket b >= 1 is below bucket_ceiling(b); k_tile_raster walks a tile's
 // buckets in order and stops as soon as every pixel of the tile holds a winner at least that near.
+// 128 buckets (round 6; 32 before: half-octaves): the early-out stops sooner and a record-free entry's
+// row-cull bound (its bucket's ceiling) is tighter -- stress scene, one MI355X, kernels serialised
+// (profiles/r06_depth_buckets_ab.txt): k_tile_raster<128u> 492 -> 475 (64) -> 457 us, device-resident
+// frames 1 160 -> 1 185 -> 1 204 fps, part 0 of 8's fragment stage 128 -> 120 us.  The bins hold
+// 256 entries per (tile, bucket) at first either way (4.2 GB for the four buffer sets at 4K).
 #ifndef S3R_DEPTH_BUCKETS
-#define S3R_DEPTH_BUCKETS 32
+#define S3R_DEPTH_BUCKETS 128
 #endif
 constexpr uint32_t kDepthBuckets = S3R_DEPTH_BUCKETS;
-constexpr uint32_t kBucketTop = 0x41200000u >> 22;  // bits(10.0f) >> 22
+static_assert(kDepthBuckets == 32 || kDepthBuckets == 64 || kDepthBuckets == 128, "16 octaves in 2, 4 or 8 buckets each");
+constexpr uint32_t kBucketShift = kDepthBuckets == 32 ? 22u : kDepthBuckets == 64 ? 21u : 20u;   // bits below the bucket
+constexpr uint32_t kBucketTop = 0x41200000u >> kBucketShift;       // bits(10.0f) >> shift
 __device__ __forceinline__ uint32_t depth_bucket(uint32_t zb_bits) {
-    const int b = (int)kBucketTop - (int)(zb_bits >> 22);
+    const int b = (int)kBucketTop - (int)(zb_bits >> kBucketShift);
     return (uint32_t)min(max(b, 0), (int)kDepthBuckets - 1);
 }
 // bits of an upper bound (exclusive) of every bound in bucket b (b = 0: none)
 __device__ __forceinline__ uint32_t bucket_ceiling(uint32_t b) {
-    return b == 0 ? 0xFFFFFFFFu : (kBucketTop - b + 1u) << 22;
+    return b == 0 ? 0xFFFFFFFFu : (kBucketTop - b + 1u) << kBucketShift;
 }
 
 // 48 B per live slot: the box, the depth bound, 1/z per corner and the three raster corners (x, y);
@@ -1588,7 +1595,7 @@ __device__ __forceinline__ TileSpan box_tiles(uint32_t bt, uint32_t by, uint32_t
 __device__ __forceinline__ uint32_t tile_box(uint32_t bx, uint32_t zb, uint32_t xoff) {
     return (((bx & 0xFFFFu) + xoff) / kTileW) | ((((bx >> 16) + xoff) / kTileW) << 12) | (depth_bucket(zb) << 24);
 }
-static_assert(kDepthBuckets <= 64, "bucket field of a packed tile box");
+static_assert(kDepthBuckets <= 128, "bucket field of a packed tile box (never the dead box's 255)");
 
 // Every lane adds 1 to counter[key] for each tile of its span (or nothing); lanes of the wave with
 // the same key share one atomic.  With `list`, the returned positions place `slot` in the lists.
@@ -2403,14 +2410,27 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
         // counts reset for the set's next frame once read.  An overflowed frame (ctr[5]) renders
         // nothing: it is binned again with larger bins (render_api.cpp)
         if (tid < 64u) {
-            const uint32_t c = tid < kDepthBuckets ? counts[s0 + tid] : 0u;
-            if (tid < kDepthBuckets) counts[s0 + tid] = 0u;
-            uint32_t inc = c;
+            constexpr uint32_t kPB = kDepthBuckets > 64u ? kDepthBuckets / 64u : 1u;   // buckets per lane
+            uint32_t c[kPB], sum = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < kPB; e++) {
+                const uint32_t b = tid * kPB + e;
+                c[e] = b < kDepthBuckets ? counts[s0 + b] : 0u;
+                if (b < kDepthBuckets) counts[s0 + b] = 0u;
+                sum += c[e];
+            }
+            uint32_t inc = sum;
             for (uint32_t o = 1; o < 64u; o <<= 1) {
                 const uint32_t v = (uint32_t)__shfl_up((int)inc, o);
                 if (tid >= o) inc += v;
             }
-            if (tid < kDepthBuckets) ls.bstart[tid] = inc - c;
+            uint32_t st = inc - sum;
+#pragma unroll
+            for (uint32_t e = 0; e < kPB; e++) {
+                const uint32_t b = tid * kPB + e;
+                if (b < kDepthBuckets) ls.bstart[b] = st;
+                st += c[e];
+            }
             if (tid == 63u) ls.zwave[0] = ctr[5] ? 0u : inc;       // (zwave: free until the first stage)
         }
         __syncthreads();
@@ -2435,16 +2455,15 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
             {                                            // the entry's depth bucket (its bound's ceiling)
                 uint32_t bb = 0;
 #pragma unroll
-                for (uint32_t step = 16; step >= 1u; step >>= 1)
+                for (uint32_t step = kDepthBuckets / 2u; step >= 1u; step >>= 1)
                     if (ls.bstart[bb + step] <= c + tid) bb += step;
                 b_nx = bb;
             }
             if (bin_cap) {
                 const uint32_t v = c + tid;
                 uint32_t b = 0;                                  // the bucket holding entry v
-                static_assert(kDepthBuckets == 32, "the bucket search covers 32 buckets");
 #pragma unroll
-                for (uint32_t step = 16; step >= 1u; step >>= 1)
+                for (uint32_t step = kDepthBuckets / 2u; step >= 1u; step >>= 1)
                     if (ls.bstart[b + step] <= v) b += step;
                 s_nx = list[(size_t)(s0 + b) * bin_cap + (v - ls.bstart[b])];
 #ifdef S3R_BOUNDS
@@ -2503,7 +2522,9 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
             // first): if every pixel of the tile already holds a winner at least as near as that
             // bucket's ceiling, no listed triangle from here on can win a pixel (strict '>', render.cpp:364)
             uint32_t b = 0;
-            for (uint32_t k = 1; k < kDepthBuckets; k++) b = ls.bstart[k] <= c0 ? k : b;
+#pragma unroll
+            for (uint32_t step = kDepthBuckets / 2u; step >= 1u; step >>= 1)
+                if (ls.bstart[b + step] <= c0) b += step;
             uint32_t zt = ls.zwave[0];
             for (uint32_t w = 1; w < kTileThreads / 64u; w++) zt = min(zt, ls.zwave[w]);
 #if !(defined(S3R_TNOSKIP) && S3R_TNOSKIP)
