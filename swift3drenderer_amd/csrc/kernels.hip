@@ -2080,6 +2080,15 @@ __global__ void __launch_bounds__(256) k_tile_setup(const float4 *__restrict__ v
             }
         }
         wave_append_u32(clip, b0 + j, clipq + b0, nclip);
+#ifdef S3R_STATS
+        {   // triangles set up live (whole frames: the aggregated binning), and the waves' lane slots
+            const uint64_t lm = __ballot(live_t), am = __ballot(j < n);
+            if ((threadIdx.x & 63u) == 0u && am) {
+                atomicAdd(&g_stats[8], (unsigned long long)__builtin_popcountll(lm));
+                atomicAdd(&g_stats[9], (unsigned long long)__builtin_popcountll(am));
+            }
+        }
+#endif
         if (aggregate)
             bin_agg(agg, slot_span(live_t, ts, band, nparts, part, xoff), t | kNoRecBit, tiles_x, counts, tbin, bin_cap,
                     ctr + 4);

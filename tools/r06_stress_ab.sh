@@ -1,8 +1,8 @@
 #!/bin/bash
-# Config 5 A/B: the product library against build/librender_$AB.so -- tile parity of the product, then
+# Config 5 A/B: the product library against build/librender_<tag>.so for each tag in $AB -- tile parity of the product, then
 # two alternations of part 0 of 8 (135-row band), the delivered stress bench line and the serialised
-# kernel times.  Usage: AB=<tag> bash tools/r06_stress_ab.sh
-OUT=gpurun_out/sab_$AB; mkdir -p $OUT; export TMPDIR=/tmp; D=/tmp/s3r_stress.bin
+# kernel times.  Usage: AB='<tag> [<tag> ...]' bash tools/r06_stress_ab.sh
+OUT=gpurun_out/sab_${AB// /_}; mkdir -p $OUT; export TMPDIR=/tmp; D=/tmp/s3r_stress.bin
 step() { local name=$1 secs=$2; shift 2; echo "== $name"; timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "   rc=$rc"; tail -n 2 "$OUT/$name.log"; return $rc; }
 step tiles_prod 300 python3 -u -m pytest tests/test_tiles.py -m gpu -x -q -s --timeout 200 --timeout-method thread || exit 1
 step data 300 python3 -c "from swift3drenderer_amd import stress; stress.write_named('icosa-stress', '$D')" || exit 1
@@ -14,11 +14,11 @@ for i in 1 2; do
     step k_${v}_$i 300 env ${L:+S3R_LIB=$L} S3R_SERIAL=1 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k_${v}_$i -o run -- python3 tools/overhead_probe.py --scene icosa-stress --pose P_id --data $D --steps 20 || exit 1
   done
 done
-python3 - "$OUT" "$AB" <<'PY'
+python3 - "$OUT" $AB <<'PY'
 import json, glob, csv, sys
-OUT, AB = sys.argv[1], sys.argv[2]
+OUT, AB = sys.argv[1], sys.argv[2:]
 for i in (1, 2):
-    for v in ('prod', AB):
+    for v in ['prod'] + AB:
         b=[json.loads(l) for l in open(f'{OUT}/bench_{v}_{i}.log') if l.startswith('{')][-1]
         p=[json.loads(l) for l in open(f'{OUT}/part8_{v}_{i}.log') if l.startswith('{')][-1]
         st=glob.glob(f'{OUT}/k_{v}_{i}/**/run_kernel_stats.csv', recursive=True)

@@ -34,6 +34,7 @@ def main():
     print(f'resolve: foreground pixels {out[2]}, runs of one winner along a row {out[3]} '
           f'({out[2] / max(out[3], 1):.2f} px per run), wave setup rounds run-shared {out[4]} of {4 * out[5]} '
           f'per-pixel (waves {out[5]}, most runs in one wave {out[6]})')
+    print(f'setup: live triangles {out[8]} of {out[9]} set up ({100.0 * out[8] / max(out[9], 1):.1f} %)')
     r.shutdown()
 
 
