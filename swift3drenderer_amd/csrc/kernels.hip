@@ -1941,61 +1941,19 @@ __device__ __forceinline__ TileSpan slot_span(bool live, const TriSetup &ts, uin
     return sp;
 }
 // One iteration's entries of the whole workgroup (every thread calls it, with n = 0 for none):
-// entry k of lane's span holds `slot`.  Four barriers; the table is left empty.  Entries go in
-// rounds k of the wave's spans, and a run of adjacent lanes with one key at round k (consecutive
-// triangles of a mesh share tiles) takes ONE table insert and LDS add for the run, from its head; the
-// run's lanes place their entries at the head's position + their rank in the run.
-#ifndef S3R_AGG_RUNS
-#define S3R_AGG_RUNS 1
-#endif
-struct AggRun { uint32_t key, leader, rank, cnt; bool act, head; };
-__device__ __forceinline__ AggRun agg_run(const TileSpan &sp, uint32_t k, uint32_t tiles_x, uint32_t lane) {
-    AggRun r;
-    r.act = k < sp.n;
-    r.key = r.act ? span_key(sp, k, tiles_x) : 0xFFFFFFFFu;
-    const uint32_t prevk = (uint32_t)__shfl_up((int)r.key, 1);
-    r.head = r.act && (lane == 0u || prevk != r.key);
-    const uint64_t heads = __ballot(r.head);
-    const uint64_t stops = heads | ~__ballot(r.act);              // a run ends at a head or an idle lane
-    const uint64_t upto = (2ull << lane) - 1ull;                   // lanes <= this one
-    r.leader = r.act ? 63u - (uint32_t)__builtin_clzll(heads & upto) : lane;
-    r.rank = lane - r.leader;
-    const uint64_t after = stops & ~upto;
-    r.cnt = r.head ? (after ? (uint32_t)__builtin_ctzll(after) : 64u) - lane : 0u;
-    return r;
-}
+// entry k of lane's span holds `slot`.  Three barriers; the table is left empty.
 __device__ void bin_agg(BinAgg &a, const TileSpan &sp, uint32_t slot, uint32_t tiles_x, uint32_t *__restrict__ counts,
                         uint32_t *__restrict__ tbin, uint32_t bin_cap, uint32_t *__restrict__ ovf) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t rounds = sp.n;
-    if (S3R_AGG_RUNS)
-        for (int o = 32; o > 0; o >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, o));
     // count
-    for (uint32_t k = 0; k < rounds; k++) {
-        if (S3R_AGG_RUNS) {
-            const AggRun r = agg_run(sp, k, tiles_x, lane);
-            uint32_t h = kAggFull, b = 0;
-            if (r.head) {
-                h = agg_insert(a, r.key);
-                if (h != kAggFull) atomicAdd(&a.cnt[h], r.cnt);
-                else b = atomicAdd(&counts[r.key], r.cnt);          // table full: the run on its own
-            }
-            h = (uint32_t)__shfl((int)h, (int)r.leader);
-            b = (uint32_t)__shfl((int)b, (int)r.leader) + r.rank;
-            if (r.act && h == kAggFull) {
-                if (b < bin_cap) tbin[(size_t)r.key * bin_cap + b] = slot;
-                else atomicMax(ovf, b + 1u);
-            }
-        } else if (k < sp.n) {
-            const uint32_t key = span_key(sp, k, tiles_x);
-            const uint32_t h = agg_insert(a, key);
-            if (h != kAggFull) {
-                atomicAdd(&a.cnt[h], 1u);
-            } else {                                     // table full: this entry on its own
-                const uint32_t b = atomicAdd(&counts[key], 1u);
-                if (b < bin_cap) tbin[(size_t)key * bin_cap + b] = slot;
-                else atomicMax(ovf, b + 1u);
-            }
+    for (uint32_t k = 0; k < sp.n; k++) {
+        const uint32_t key = span_key(sp, k, tiles_x);
+        const uint32_t h = agg_insert(a, key);
+        if (h != kAggFull) {
+            atomicAdd(&a.cnt[h], 1u);
+        } else {                                         // table full: this entry on its own
+            const uint32_t b = atomicAdd(&counts[key], 1u);
+            if (b < bin_cap) tbin[(size_t)key * bin_cap + b] = slot;
+            else atomicMax(ovf, b + 1u);
         }
     }
     __syncthreads();
@@ -2010,24 +1968,12 @@ __device__ void bin_agg(BinAgg &a, const TileSpan &sp, uint32_t slot, uint32_t t
     }
     __syncthreads();
     // write the runs
-    for (uint32_t k = 0; k < rounds; k++) {
-        if (S3R_AGG_RUNS) {
-            const AggRun r = agg_run(sp, k, tiles_x, lane);
-            uint32_t h = kAggFull, pos = 0;
-            if (r.head) {
-                h = agg_find(a, r.key);
-                if (h != kAggFull) pos = a.base[h] + atomicAdd(&a.cnt[h], r.cnt);
-            }
-            h = (uint32_t)__shfl((int)h, (int)r.leader);
-            pos = (uint32_t)__shfl((int)pos, (int)r.leader) + r.rank;
-            if (r.act && h != kAggFull && pos < bin_cap) tbin[(size_t)r.key * bin_cap + pos] = slot;
-        } else if (k < sp.n) {
-            const uint32_t key = span_key(sp, k, tiles_x);
-            const uint32_t h = agg_find(a, key);
-            if (h == kAggFull) continue;                 // (written above)
-            const uint32_t pos = a.base[h] + atomicAdd(&a.cnt[h], 1u);
-            if (pos < bin_cap) tbin[(size_t)key * bin_cap + pos] = slot;
-        }
+    for (uint32_t k = 0; k < sp.n; k++) {
+        const uint32_t key = span_key(sp, k, tiles_x);
+        const uint32_t h = agg_find(a, key);
+        if (h == kAggFull) continue;                     // (written above)
+        const uint32_t pos = a.base[h] + atomicAdd(&a.cnt[h], 1u);
+        if (pos < bin_cap) tbin[(size_t)key * bin_cap + pos] = slot;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nu; i += blockDim.x) {
