@@ -2293,8 +2293,10 @@ constexpr uint32_t kDeferPixel = 0xFFFFFFFFu;           // (never a pixel: 0x00R
 // values k_tile_setup computed); a clip-appended or near-plane-crossing winner needs its full setup
 // (slot_setup, the clip) -- with DEFER the pixel returns kDeferPixel for k_tile_resolve_deferred
 // instead (rare, and the clip's registers stay out of the caller).
+// vi (RC): the winner's three vertex indices staged in LDS by the caller, or null (read from the scene).
 template <bool DEFER, bool RC = false>
-__device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned long long k, uint32_t x, uint32_t y) {
+__device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned long long k, uint32_t x, uint32_t y,
+                                                  const uint32_t *vi = nullptr) {
     if (!k) return kBackground;
     const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
     const float ooz = u2f((uint32_t)(k >> 32));
@@ -2310,7 +2312,7 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
             Vert d[3];
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                project_corner(sc.vtx[sc.vidx[3 * t + c]], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[c]);
+                project_corner(sc.vtx[vi ? vi[c] : sc.vidx[3 * t + c]], sc.m, sc.factor, sc.sw / 2, sc.sh / 2, d[c]);
                 near_cut = near_cut || d[c].rv.z < kNear;
             }
             if (s >= sc.ntri || near_cut) {
@@ -2328,7 +2330,7 @@ __device__ __forceinline__ uint32_t resolve_pixel(const ShadeScene &sc, unsigned
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 const uint32_t ai = sc.aidx[3 * t + c];
-                d[c].cv = mat_mul(sc.m, sc.vtx[sc.vidx[3 * t + c]]);              // (as project_corner: :286)
+                d[c].cv = mat_mul(sc.m, sc.vtx[vi ? vi[c] : sc.vidx[3 * t + c]]);   // (as project_corner: :286)
                 d[c].n = mat_mul(sc.m, sc.nrm[ai]);
                 d[c].pay = sc.pay[ai];
             }
@@ -2721,6 +2723,27 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
     }
 #endif
     {
+#ifndef S3R_RESOLVE_VIX
+#define S3R_RESOLVE_VIX 1
+#endif
+        // the winners' vertex indices of all the tile's pixels loaded at once into LDS (the staging
+        // arrays, free now): each pixel's chain of dependent loads then starts at its corners
+        // (stages of 128 triangles and more: the staging arrays hold the tile's 1 024 x 3 indices)
+        constexpr bool kVix = S3R_RESOLVE_VIX &&
+            offsetof(TileShared<STAGE>, wsum) - offsetof(TileShared<STAGE>, ws) >= kTileH * kTileW * 3u * 4u;
+        uint32_t *const vix = reinterpret_cast<uint32_t *>(&ls.ws[0][0]);
+        if (kVix) {
+#pragma unroll
+            for (uint32_t q = 0; q < kTileH * kTileW / kTileThreads; q++) {
+                const uint32_t i = tid + q * kTileThreads, rr = i / kTileW, cc = i % kTileW;
+                const unsigned long long k = tr0 + rr <= tr1 && lx0 + cc <= lx1 ? ls.key[rr * kKeyStride + cc] : 0ull;
+                const uint32_t s = 0xFFFFFFFFu - (uint32_t)k;
+                uint32_t v0 = 0, v1 = 0, v2 = 0;
+                if (k && s < sc.ntri) { v0 = sc.vidx[3 * s]; v1 = sc.vidx[3 * s + 1]; v2 = sc.vidx[3 * s + 2]; }
+                vix[3 * i] = v0; vix[3 * i + 1] = v1; vix[3 * i + 2] = v2;
+            }
+            __syncthreads();
+        }
         for (uint32_t i = tid; i < kTileH * kTileW; i += kTileThreads) {   // (wave-uniform trip count)
             const uint32_t rr = i / kTileW, cc = i % kTileW;
             const uint32_t lr = tr0 + rr, x = lx0 + cc;
@@ -2731,7 +2754,7 @@ __global__ void __launch_bounds__(kTileThreads, STAGE <= 128u ? S3R_TOCC : 1) k_
 #if defined(S3R_TABLATE) && (S3R_TABLATE & 8)
             if (in) v = (uint32_t)k & 0xFFFFFFu;                // ablation: no resolve (timing only)
 #else
-            if (in) v = resolve_pixel<true, true>(sc, k, x, y);
+            if (in) v = resolve_pixel<true, true>(sc, k, x, y, kVix ? vix + 3 * i : nullptr);
 #endif
             const size_t idx = frame_rows ? (size_t)y * W + x : (size_t)lr * W + x;
 #ifdef S3R_BOUNDS
