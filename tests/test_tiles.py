@@ -492,7 +492,7 @@ def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, b
     frames overflow: synchronous frames (updateAndRender, one device and three parts) are binned
     again after the frame, asynchronous ones (s3r_render_bands) before their fragment stage.  With a
     1-MiB budget (S3R_TILE_BIN_BUDGET_MB) the grown bins (cap 4) or the first ones (cap 256: 640x480
-    is 9 600 (tile, bucket)s, 9.8 MB for four buffer sets) do not fit: the device falls back to the
+    is 38 400 (tile, bucket)s at 128 depth buckets, 39 MB for four buffer sets) do not fit: the device falls back to the
     lists, mid-frame or from the start."""
     import torch
     from oracle.oracle import OracleRenderer
