@@ -484,16 +484,16 @@ def test_tile_line_offsets_match_oracle(gpu_renderer, icosa_dir, devices):
         r.configure_devices([])
 
 
-@pytest.mark.parametrize('bin_cap,budget_mb',[('256', ''), ('4', ''), ('4', '1'), ('256', '1')])
+@pytest.mark.parametrize('bin_cap,budget_mb',[('256', ''), ('4', ''), ('4', '4'), ('256', '1')])
 @pytest.mark.parametrize('devices', [[0], [0, 0, 0]])
 def test_tile_bins_match_oracle(gpu_renderer, icosa_dir, monkeypatch, bin_cap, budget_mb, devices):
     """Bins mode (the default): the setup writes each slot straight into fixed-capacity bins of its
     (tile, bucket)s -- no scan, no fill pass.  A tiny first capacity (S3R_TILE_BIN_CAP=4) makes
     frames overflow: synchronous frames (updateAndRender, one device and three parts) are binned
     again after the frame, asynchronous ones (s3r_render_bands) before their fragment stage.  With a
-    1-MiB budget (S3R_TILE_BIN_BUDGET_MB) the grown bins (cap 4) or the first ones (cap 256: 640x480
-    is 38 400 (tile, bucket)s at 128 depth buckets, 39 MB for four buffer sets) do not fit: the device falls back to the
-    lists, mid-frame or from the start."""
+    small budget (S3R_TILE_BIN_BUDGET_MB) the bins grown from cap 4 (4 MiB: 640x480 is 38 400 (tile,
+    bucket)s at 128 depth buckets, 2.5 MB for four buffer sets at cap 4) or the first ones at cap 256
+    (1 MiB: 39 MB) do not fit: the device falls back to the lists, mid-frame or from the start."""
     import torch
     from oracle.oracle import OracleRenderer
     monkeypatch.setenv('S3R_TILE_BINS', '1')
